@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""bench.py -- Boda per-op conv/SGEMM hot path on MI355X.
+
+Metric (BASELINE.json): per-op GFLOPS and % fp32 roofline on sgemm-ops-full +
+conv-ops (AlexNet/NiN/GoogLeNet). A "step" is one pass over the workload's op
+list, one main-kernel launch per op, inputs resident in HBM (generated on the
+device with the reference's gen_data mode 5 before the timed region).
+
+  value       = sum of algorithmic flops of every op launched on every rank in
+                the timed steps / max-over-ranks wall time    [GFLOP/s]
+  per_set     = per op-list aggregate in the reference's own convention:
+                sum flops / sum event-timed kernel seconds (src/rtc_prof.cc:104-124),
+                plus sum(roofline time) / sum(kernel time)
+  roofline    = the dominant kernel (most event time): algorithmic flops per launch
+                / its average launch duration (HIP events on its stream), vs fp32 peak
+  cpu_baseline= the oracle's fp32 OpenMP CPU implementation (kind "port") on a
+                bounded sample, rank 0 at N=1 only
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+ops are independent so there is no data-path collective; every
+rank runs one full copy of the op list on its own GPU (weak scaling), a gloo
+barrier brackets the timed region and the max wall time over ranks is used.
+--strong instead shards ONE op list over the ranks (greedy LPT on roofline time).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "boda-1_amd"))
+sys.path.insert(0, ROOT)
+
+import boda_hip  # noqa: E402
+from boda_hip import ops, runner  # noqa: E402
+
+OPS_DIR = os.path.join(ROOT, "tests", "golden", "ops")
+SETS = {
+    "sgemm-full": "sgemm-ops-full.txt",
+    "sgemm-small": "sgemm-ops-small.txt",
+    "sgemm-tiny": "sgemm-ops-tiny.txt",
+    "conv": "conv-ops-1-5-20-nin-alex-gn.txt",
+    "op-sigs": "op_sigs_full.txt",
+}
+DEFAULT_SETS = ["sgemm-full", "conv"]
+
+
+def load_sets(names):
+    shapes, tags = [], []
+    for n in names:
+        o, _ = ops.read_ops(os.path.join(OPS_DIR, SETS[n]))
+        for op in o:
+            shapes.append(ops.shape_of(op))
+            tags.append(n)
+    return shapes, tags
+
+
+def lpt_partition(costs, n):
+    """Greedy longest-processing-time assignment of items to n bins; returns a list of index lists."""
+    bins = [[] for _ in range(n)]
+    load = [0.0] * n
+    for i in sorted(range(len(costs)), key=lambda i: -costs[i]):
+        j = min(range(n), key=lambda j: load[j])
+        bins[j].append(i)
+        load[j] += costs[i]
+    return [sorted(b) for b in bins]
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(budget_s):
+    """Time the oracle's fp32 OpenMP CPU path on a bounded sample of the same workload."""
+    from oracle import oracle as orc
+    conv, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["conv"]))
+    sg, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["sgemm-small"]))
+    sample = [ops.shape_of(o) for o in conv if ops.shape_of(o).B in (1, 5)]
+    sample += [ops.shape_of(o) for o in sg if ops.shape_of(o).M <= 1024]
+    flops = secs = 0.0
+    done = 0
+    for s in sample:
+        if isinstance(s, ops.SgemmShape):
+            a, b = orc.gen_sgemm(s.M, s.N, s.K, 5)
+            t0 = time.perf_counter()
+            orc.sgemm_ref(a, b, s.M, s.N, s.K, fast=True)
+        else:
+            i, f, b = orc.gen_conv(s, 5)
+            t0 = time.perf_counter()
+            orc.conv_ref(i, f, b, s, 1, fast=True)
+        secs += time.perf_counter() - t0
+        flops += s.flops()
+        done += 1
+        if secs > budget_s:
+            break
+    return {"value": round(flops / secs / 1e9, 3), "unit": "GFLOP/s", "cores": orc.num_threads(), "kind": "port",
+            "sample": "%d of %d ops: conv-ops-1-5-20 at batch 1 and 5 + sgemm-ops-small <= 1024^3, fp32, "
+                      "%.1f GFLOP in %.1f s" % (done, len(sample), flops / 1e9, secs)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sets", default=",".join(DEFAULT_SETS))
+    ap.add_argument("--strong", action="store_true", help="shard one op list over the ranks (LPT)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--per-op", default="", help="write per-op event times (JSON) to this path")
+    args = ap.parse_args()
+
+    dd = Dist()
+    if dd.world != args.gpus:
+        if args.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
+    set_names = [s for s in args.sets.split(",") if s]
+    shapes, tags = load_sets(set_names)
+    if args.strong and dd.world > 1:
+        mine = lpt_partition([runner.roofline_secs(s) for s in shapes], dd.world)[dd.rank]
+    else:
+        mine = list(range(len(shapes)))
+    my_shapes = [shapes[i] for i in mine]
+    my_tags = [tags[i] for i in mine]
+
+    dev = boda_hip.Device(dd.local_rank)
+    wl = runner.Workload(dev, my_shapes, mode=5, tags=my_tags)
+    for _ in range(args.warmup):
+        wl.step()
+    dev.sync()
+
+    events = []
+    dd.barrier()
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step(events)
+    dev.sync()
+    t1 = time.perf_counter()
+    dd.barrier()
+    elapsed = dd.max(t1 - t0)
+
+    # per-op kernel times (events on the context's stream), mean over the timed steps
+    ktime = [0.0] * len(my_shapes)
+    for i, b, e in events:
+        ktime[i] += dev.elapsed_ms(b, e) / 1e3
+    ktime = [t / args.steps for t in ktime]
+    dev.events_reset()
+
+    my_flops = sum(s.flops() for s in my_shapes)
+    total_flops = dd.sum(my_flops) * args.steps
+    value = total_flops / elapsed / 1e9
+
+    per_set = {}
+    for n in set_names:
+        idx = [i for i, t in enumerate(my_tags) if t == n]
+        if not idx:
+            continue
+        f = sum(my_shapes[i].flops() for i in idx)
+        t = sum(ktime[i] for i in idx)
+        rt = sum(runner.roofline_secs(my_shapes[i]) for i in idx)
+        per_set[n] = {"ops": len(idx), "gflop": round(f / 1e9, 3), "sum_kernel_ms": round(t * 1e3, 4),
+                      "gflops": round(f / t / 1e9, 2), "roofline_frac": round(rt / t, 4),
+                      "roofline_ms": round(rt * 1e3, 4)}
+
+    # dominant kernel: the variant with the most event time
+    by_var = {}
+    for i, s in enumerate(my_shapes):
+        kind = 0 if isinstance(s, ops.SgemmShape) else 1
+        dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
+        v = boda_hip.variant_name(kind, dims)
+        d = by_var.setdefault(v, {"t": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
+        d["t"] += ktime[i]
+        d["flops"] += s.flops()
+        d["bytes"] += s.bytes()
+        d["n"] += 1
+    dom = max(by_var, key=lambda v: by_var[v]["t"])
+    dv = by_var[dom]
+    achieved = dv["flops"] / dv["t"] / 1e12
+    roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": runner.PEAK_FP32_FLOPS / 1e12,
+            "unit": "TFLOP/s", "frac": round(achieved * 1e12 / runner.PEAK_FP32_FLOPS, 4), "traffic": None,
+            "launches_per_step": dv["n"], "avg_launch_ms": round(dv["t"] / dv["n"] * 1e3, 4),
+            "avg_flops_per_launch": dv["flops"] / dv["n"]}
+    tp = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tp):
+        try:
+            tj = json.load(open(tp))
+            if tj.get("kernel") == dom:
+                roof["traffic"] = tj.get("bytes_per_launch")
+                roof["traffic_source"] = tj.get("source")
+        except (OSError, ValueError):
+            pass
+
+    cpu = None
+    if dd.rank == 0 and dd.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_budget)
+
+    if args.per_op and dd.rank == 0:
+        with open(args.per_op, "w") as f:
+            json.dump([{"tag": my_tags[i], "dims": (my_shapes[i].as_dims() if isinstance(my_shapes[i], ops.ConvShape)
+                                                   else [my_shapes[i].M, my_shapes[i].N, my_shapes[i].K]),
+                        "kernel_ms": ktime[i] * 1e3, "gflops": my_shapes[i].flops() / ktime[i] / 1e9,
+                        "roofline_frac": runner.roofline_secs(my_shapes[i]) / ktime[i],
+                        "bound": runner.bound_of(my_shapes[i])} for i in range(len(my_shapes))], f, indent=0)
+
+    if dd.rank == 0:
+        line = {
+            "metric": "per-op GFLOPS and % fp32 roofline on sgemm-ops-full + conv-ops (AlexNet/NiN/GoogLeNet)",
+            "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": dd.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong" if (args.strong and dd.world > 1) else "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (reference gen_data mode 5, generated on device)",
+            "config": {"workload": " + ".join(SETS[n] for n in set_names) + " (one main-kernel launch per op per step)",
+                       "ops_per_gpu": len(my_shapes), "gflop_per_step_per_gpu": round(my_flops / 1e9, 3),
+                       "parallelism": ("op-shard" if args.strong else "op-replica") + "%d" % dd.world,
+                       "plat": dev.plat_tag()},
+            "per_set": per_set,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    wl.free()
+    dev.close()
+    dd.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+"""ctypes binding of libboda_hip.so (include/boda_hip.h) for tests and bench.py.
+
+The binding is thin on purpose: every call goes straight through the C-ABI a
+Boda maintainer would bind from hip_compute_t. There is no CPU
+fallback: without a gfx950 device Device() raises BodaHipError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import ops  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libboda_hip.so")
+
+BH_OK, BH_ERR, BH_UNSUP = 0, 1, 2
+GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5)
+
+# every symbol include/boda_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_destroy", "bh_plat_tag",
+           "bh_get_stream", "bh_alloc", "bh_free", "bh_memset0", "bh_h2d", "bh_d2h", "bh_sync",
+           "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
+           "bh_conv2d_fwd_nchw", "bh_variant_name"]
+
+
+class BodaHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+class UnsupportedError(BodaHipError):
+    pass
+
+
+_lib = None
+c_u32 = ctypes.c_uint32
+c_vp = ctypes.c_void_p
+
+
+def lib():
+    """Load libboda_hip.so (built in-tree by __graft_entry__.build / make)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BodaHipError(BH_ERR, "libboda_hip.so not built at %s (run __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        L.bh_last_error.restype = ctypes.c_char_p
+        L.bh_abi_version.restype = ctypes.c_int
+        L.bh_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.bh_init.argtypes = [ctypes.c_int, ctypes.POINTER(c_vp)]
+        L.bh_destroy.argtypes = [c_vp]
+        L.bh_plat_tag.argtypes = [c_vp, ctypes.c_char_p, ctypes.c_size_t]
+        L.bh_get_stream.argtypes = [c_vp, ctypes.POINTER(c_vp)]
+        L.bh_alloc.argtypes = [c_vp, ctypes.c_size_t, ctypes.POINTER(c_vp)]
+        L.bh_free.argtypes = [c_vp, c_vp]
+        L.bh_memset0.argtypes = [c_vp, c_vp, ctypes.c_size_t]
+        L.bh_h2d.argtypes = [c_vp, c_vp, c_vp, ctypes.c_size_t]
+        L.bh_d2h.argtypes = [c_vp, c_vp, c_vp, ctypes.c_size_t]
+        L.bh_sync.argtypes = [c_vp]
+        L.bh_event_record.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int)]
+        L.bh_elapsed_ms.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.bh_events_reset.argtypes = [c_vp]
+        L.bh_gen_data.argtypes = [c_vp, ctypes.c_int, c_vp, ctypes.POINTER(c_u32), c_u32, ctypes.c_float]
+        L.bh_sgemm_kmajor.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32]
+        L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
+        L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != BH_OK:
+        msg = lib().bh_last_error().decode(errors="replace")
+        raise (UnsupportedError if rc == BH_UNSUP else BodaHipError)(rc, msg)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(lib().bh_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def variant_name(op_kind, dims):
+    arr = (c_u32 * 16)(*dims)
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().bh_variant_name(op_kind, arr, buf, 256))
+    return buf.value.decode()
+
+
+class DevBuf:
+    """A device allocation owned by a Device (freed explicitly or with the Device)."""
+
+    def __init__(self, dev, ptr, nbytes):
+        self.dev, self.ptr, self.nbytes = dev, ptr, nbytes
+
+    @property
+    def nfloats(self):
+        return self.nbytes // 4
+
+    def upload(self, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        assert a.nbytes <= self.nbytes
+        _check(lib().bh_h2d(self.dev.ctx, self.ptr, a.ctypes.data, a.nbytes))
+
+    def download(self, n=None, out=None):
+        n = self.nfloats if n is None else n
+        o = np.empty(n, np.float32) if out is None else out
+        _check(lib().bh_d2h(self.dev.ctx, o.ctypes.data, self.ptr, n * 4))
+        return o
+
+    def zero(self):
+        _check(lib().bh_memset0(self.dev.ctx, self.ptr, self.nbytes))
+
+    def free(self):
+        if self.ptr:
+            _check(lib().bh_free(self.dev.ctx, self.ptr))
+            self.dev._bufs.discard(self)
+            self.ptr = None
+
+
+class Device:
+    """One bh_ctx: a gfx950 device and its stream."""
+
+    def __init__(self, device=0):
+        self.ctx = c_vp()
+        _check(lib().bh_init(device, ctypes.byref(self.ctx)))
+        self.index = device
+        self._bufs = set()
+
+    def close(self):
+        if self.ctx:
+            for b in list(self._bufs):
+                b.free()
+            _check(lib().bh_destroy(self.ctx))
+            self.ctx = c_vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def plat_tag(self):
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().bh_plat_tag(self.ctx, buf, 256))
+        return buf.value.decode()
+
+    def alloc(self, nbytes):
+        p = c_vp()
+        _check(lib().bh_alloc(self.ctx, nbytes, ctypes.byref(p)))
+        b = DevBuf(self, p.value, nbytes)
+        self._bufs.add(b)
+        return b
+
+    def alloc_floats(self, n):
+        return self.alloc(4 * int(n))
+
+    def sync(self):
+        _check(lib().bh_sync(self.ctx))
+
+    def event(self):
+        i = ctypes.c_int(0)
+        _check(lib().bh_event_record(self.ctx, ctypes.byref(i)))
+        return i.value
+
+    def elapsed_ms(self, b, e):
+        ms = ctypes.c_float(0)
+        _check(lib().bh_elapsed_ms(self.ctx, b, e, ctypes.byref(ms)))
+        return ms.value
+
+    def events_reset(self):
+        _check(lib().bh_events_reset(self.ctx))
+
+    def gen_data(self, kind, buf, dims, mode, vi=0.0):
+        d = list(dims) + [1] * (4 - len(dims))
+        arr = (c_u32 * 4)(*d)
+        _check(lib().bh_gen_data(self.ctx, kind, buf.ptr, arr, mode, vi))
+
+    def sgemm(self, a, b, c, M, N, K):
+        _check(lib().bh_sgemm_kmajor(self.ctx, a.ptr, b.ptr, c.ptr, M, N, K))
+
+    def conv(self, inp, filts, biases, out, s, relu=1):
+        _check(lib().bh_conv2d_fwd_nchw(self.ctx, inp.ptr, filts.ptr, biases.ptr if biases is not None else None,
+                                        out.ptr, s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px,
+                                        int(relu)))

@@ -1,0 +1,91 @@
+"""Per-op workload runner: the Python twin of ops-prof's profile_rcg_call
+(src/rtc_prof.cc:44-126) over the C-ABI, used by bench.py and the GPU tests.
+
+For each op: create its vars on the device (zero-filled), fill the inputs with
+the reference's gen_data (mode 5 by default) on the device, then launch the
+main kernel as often as asked, timing each launch between a pair of HIP
+events on the context's stream (the reference times exactly this: one
+main-kernel call, no data generation or layout transforms, F7).
+"""
+from dataclasses import dataclass
+
+from . import GEN_CONV_BIASES, GEN_CONV_FILTS, GEN_CONV_IN, GEN_SGEMM_A, GEN_SGEMM_B
+from .ops import ConvShape, SgemmShape
+
+# MI355X peaks (MI355X_MICROARCH.md): fp32 matrix = vector = 157.3 TFLOP/s; HBM3E 8.0 TB/s.
+PEAK_FP32_FLOPS = 157.3e12
+PEAK_HBM_BPS = 8.0e12
+
+
+def roofline_secs(shape):
+    """Per-op roofline time: max(flops / fp32 peak, algorithmic bytes / HBM peak)."""
+    return max(shape.flops() / PEAK_FP32_FLOPS, shape.bytes() / PEAK_HBM_BPS)
+
+
+def bound_of(shape):
+    return "mfma" if shape.flops() / PEAK_FP32_FLOPS >= shape.bytes() / PEAK_HBM_BPS else "hbm"
+
+
+@dataclass
+class OpVars:
+    shape: object
+    bufs: tuple
+    tag: str = ""
+
+
+class Workload:
+    def __init__(self, dev, shapes, mode=5, tags=None):
+        self.dev = dev
+        self.ops = []
+        for i, s in enumerate(shapes):
+            tag = tags[i] if tags else ""
+            if isinstance(s, SgemmShape):
+                a = dev.alloc_floats(s.K * s.M)
+                b = dev.alloc_floats(s.K * s.N)
+                c = dev.alloc_floats(s.M * s.N)
+                dev.gen_data(GEN_SGEMM_A, a, [s.K, s.M], mode)
+                dev.gen_data(GEN_SGEMM_B, b, [s.K, s.N], mode)
+                self.ops.append(OpVars(s, (a, b, c), tag))
+            elif isinstance(s, ConvShape):
+                inp = dev.alloc_floats(s.B * s.IC * s.H * s.W)
+                f = dev.alloc_floats(s.OC * s.K)
+                bi = dev.alloc_floats(s.OC)
+                o = dev.alloc_floats(s.B * s.OC * s.OH * s.OW)
+                dev.gen_data(GEN_CONV_IN, inp, [s.B, s.IC, s.H, s.W], mode)
+                dev.gen_data(GEN_CONV_FILTS, f, [s.OC, s.IC, s.KY, s.KX], mode)
+                dev.gen_data(GEN_CONV_BIASES, bi, [s.OC], mode)
+                self.ops.append(OpVars(s, (inp, f, bi, o), tag))
+            else:
+                raise TypeError(s)
+        dev.sync()
+
+    def launch(self, i):
+        v = self.ops[i]
+        s = v.shape
+        if isinstance(s, SgemmShape):
+            a, b, c = v.bufs
+            self.dev.sgemm(a, b, c, s.M, s.N, s.K)
+        else:
+            inp, f, bi, o = v.bufs
+            self.dev.conv(inp, f, bi, o, s, 1)
+
+    def output(self, i):
+        return self.ops[i].bufs[-1].download()
+
+    def step(self, timed_events=None):
+        """One pass over every op (one main-kernel launch each). With timed_events (a list),
+        appends (op index, begin event, end event)."""
+        for i in range(len(self.ops)):
+            if timed_events is not None:
+                b = self.dev.event()
+                self.launch(i)
+                e = self.dev.event()
+                timed_events.append((i, b, e))
+            else:
+                self.launch(i)
+
+    def free(self):
+        for v in self.ops:
+            for b in v.bufs:
+                b.free()
+        self.ops = []

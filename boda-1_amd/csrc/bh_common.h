@@ -1,0 +1,59 @@
+// bh_common.h -- internal declarations shared by the libboda_hip.so sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "boda_hip.h"
+
+struct bh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipDeviceProp_t prop{};
+  std::vector<hipEvent_t> events;  // pool; ids index into it
+  int events_used = 0;
+};
+
+namespace bh {
+
+int fail(int code, const std::string &msg);  // records thread-local message, returns code
+int ok();                                    // clears nothing, returns BH_OK
+
+// Kernel launch checks (hipGetLastError after each launch).
+int check_launch(const char *what);
+
+// Magic-number unsigned division for 0 <= n < 2^31, 1 <= d < 2^31:
+// q = (umulhi(n, m) + n) >> s.
+struct fastdiv {
+  uint32_t d, m, s;
+};
+inline fastdiv make_fastdiv(uint32_t d) {
+  fastdiv f{d, 0, 0};
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+}  // namespace bh
+
+#define BH_HIP(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) return bh::fail(BH_ERR, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define BH_CHECK_CTX(c) \
+  do { if (!(c)) return bh::fail(BH_ERR, "null bh_ctx"); } while (0)
+
+// ---- internal entry points implemented in the kernel sources ----
+namespace bh {
+int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi);
+int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t M, uint32_t N, uint32_t K);
+int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *biases, float *out,
+                uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
+                uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu);
+std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
+std::string conv_variant(const uint32_t *d);
+}  // namespace bh

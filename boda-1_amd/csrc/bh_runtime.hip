@@ -1,0 +1,209 @@
+// bh_runtime.hip -- device context, vars, copies, events and the extern "C"
+// surface of libboda_hip.so (declared in include/boda_hip.h).
+//
+// Mirrors the contract of Boda's nvrtc_compute_t (src/nvrtc_util.cc:174-395):
+// one device per context, zero-filled var allocation (:80-84), an event pair
+// around every timed call (:289-298, :367-381), durations in milliseconds
+// (src/rtc_compute.H:66-71). Unlike the reference (default stream 0), each
+// context owns a non-blocking stream so several contexts / host threads can
+// drive several GPUs of one node independently.
+#include "bh_common.h"
+#include <cstdio>
+#include <cstring>
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+namespace bh {
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+int ok() { return BH_OK; }
+int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BH_ERR, std::string("launch of ") + what + " failed: " + hipGetErrorString(e));
+  return BH_OK;
+}
+}  // namespace bh
+
+extern "C" {
+
+int bh_abi_version(void) { return BH_ABI_VERSION; }
+
+const char *bh_last_error(void) { return g_last_error.c_str(); }
+
+int bh_device_count(int *count) {
+  if (!count) return bh::fail(BH_ERR, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return BH_OK;
+}
+
+int bh_init(int device, bh_ctx **out) {
+  if (!out) return bh::fail(BH_ERR, "null ctx out-pointer");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return bh::fail(BH_ERR, "no HIP device available (libboda_hip has no CPU fallback)");
+  if (device < 0 || device >= n) return bh::fail(BH_ERR, "device index out of range");
+  bh_ctx *c = new bh_ctx();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipGetDeviceProperties(&c->prop, device);
+  if (e == hipSuccess && std::strncmp(c->prop.gcnArchName, "gfx950", 6) != 0) {
+    std::string arch = c->prop.gcnArchName;
+    delete c;
+    return bh::fail(BH_ERR, "device is " + arch + "; libboda_hip is built for gfx950 (MI355X) only");
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return bh::fail(BH_ERR, std::string("bh_init: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return BH_OK;
+}
+
+int bh_destroy(bh_ctx *c) {
+  BH_CHECK_CTX(c);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return BH_OK;
+}
+
+int bh_plat_tag(bh_ctx *c, char *buf, size_t n) {
+  BH_CHECK_CTX(c);
+  if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
+  std::snprintf(buf, n, "hip:%s:%s", c->prop.name, c->prop.gcnArchName);
+  return BH_OK;
+}
+
+int bh_get_stream(bh_ctx *c, void **s) {
+  BH_CHECK_CTX(c);
+  if (!s) return bh::fail(BH_ERR, "null out");
+  *s = (void *)c->stream;
+  return BH_OK;
+}
+
+int bh_alloc(bh_ctx *c, size_t bytes, void **p) {
+  BH_CHECK_CTX(c);
+  if (!p) return bh::fail(BH_ERR, "null out");
+  *p = nullptr;
+  BH_HIP(hipSetDevice(c->device));
+  void *d = nullptr;
+  BH_HIP(hipMalloc(&d, bytes ? bytes : 16));
+  hipError_t e = hipMemsetAsync(d, 0, bytes ? bytes : 16, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return bh::fail(BH_ERR, std::string("bh_alloc zero-fill: ") + hipGetErrorString(e));
+  }
+  *p = d;
+  return BH_OK;
+}
+
+int bh_free(bh_ctx *c, void *p) {
+  BH_CHECK_CTX(c);
+  BH_HIP(hipSetDevice(c->device));
+  BH_HIP(hipStreamSynchronize(c->stream));
+  BH_HIP(hipFree(p));
+  return BH_OK;
+}
+
+int bh_memset0(bh_ctx *c, void *p, size_t bytes) {
+  BH_CHECK_CTX(c);
+  BH_HIP(hipMemsetAsync(p, 0, bytes, c->stream));
+  return BH_OK;
+}
+
+int bh_h2d(bh_ctx *c, void *d, const void *h, size_t bytes) {
+  BH_CHECK_CTX(c);
+  // synchronous w.r.t. the host buffer (caller may free it on return)
+  BH_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+  BH_HIP(hipStreamSynchronize(c->stream));
+  return BH_OK;
+}
+
+int bh_d2h(bh_ctx *c, void *h, const void *d, size_t bytes) {
+  BH_CHECK_CTX(c);
+  BH_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+  BH_HIP(hipStreamSynchronize(c->stream));
+  return BH_OK;
+}
+
+int bh_sync(bh_ctx *c) {
+  BH_CHECK_CTX(c);
+  BH_HIP(hipStreamSynchronize(c->stream));
+  return BH_OK;
+}
+
+int bh_event_record(bh_ctx *c, int *id) {
+  BH_CHECK_CTX(c);
+  if (!id) return bh::fail(BH_ERR, "null out");
+  if (c->events_used == (int)c->events.size()) {
+    hipEvent_t ev;
+    BH_HIP(hipEventCreate(&ev));
+    c->events.push_back(ev);
+  }
+  BH_HIP(hipEventRecord(c->events[c->events_used], c->stream));
+  *id = c->events_used++;
+  return BH_OK;
+}
+
+int bh_elapsed_ms(bh_ctx *c, int b, int e, float *ms) {
+  BH_CHECK_CTX(c);
+  if (!ms) return bh::fail(BH_ERR, "null out");
+  if (b < 0 || e < 0 || b >= c->events_used || e >= c->events_used) return bh::fail(BH_ERR, "bad event id");
+  BH_HIP(hipEventSynchronize(c->events[e]));
+  BH_HIP(hipEventElapsedTime(ms, c->events[b], c->events[e]));
+  return BH_OK;
+}
+
+int bh_events_reset(bh_ctx *c) {
+  BH_CHECK_CTX(c);
+  c->events_used = 0;
+  return BH_OK;
+}
+
+int bh_gen_data(bh_ctx *c, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi) {
+  BH_CHECK_CTX(c);
+  if (!dst || !dims) return bh::fail(BH_ERR, "null argument");
+  return bh::launch_gen_data(c, kind, dst, dims, mode, vi);
+}
+
+int bh_sgemm_kmajor(bh_ctx *c, const float *a, const float *b, float *cc, uint32_t M, uint32_t N, uint32_t K) {
+  BH_CHECK_CTX(c);
+  if (!a || !b || !cc) return bh::fail(BH_ERR, "null tensor");
+  if (!M || !N || !K) return bh::fail(BH_UNSUP, "sgemm: zero-sized dimension");
+  return bh::launch_sgemm(c, a, b, cc, M, N, K);
+}
+
+int bh_conv2d_fwd_nchw(bh_ctx *c, const float *in, const float *filts, const float *biases, float *out,
+                       uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
+                       uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
+  BH_CHECK_CTX(c);
+  if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
+    return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
+  if (H + 2 * py < KY || W + 2 * px < KX) return bh::fail(BH_UNSUP, "conv: padded input smaller than kernel");
+  return bh::launch_conv(c, in, filts, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
+}
+
+int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
+  if (!dims || !buf || !n) return bh::fail(BH_ERR, "null argument");
+  std::string s;
+  if (op == 0) s = bh::sgemm_variant(dims[0], dims[1], dims[2]);
+  else if (op == 1) s = bh::conv_variant(dims);
+  else return bh::fail(BH_ERR, "unknown op kind");
+  std::snprintf(buf, n, "%s", s.c_str());
+  return BH_OK;
+}
+
+}  // extern "C"
