@@ -22,7 +22,7 @@ GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5
 EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_destroy", "bh_plat_tag",
            "bh_get_stream", "bh_alloc", "bh_free", "bh_memset0", "bh_h2d", "bh_d2h", "bh_sync",
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
-           "bh_conv2d_fwd_nchw", "bh_variant_name"]
+           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name"]
 
 
 class BodaHipError(RuntimeError):
@@ -67,6 +67,8 @@ def lib():
         L.bh_sgemm_kmajor.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32]
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
+        L.bh_tune_set.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.bh_tune_cfg_name.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -88,6 +90,16 @@ def variant_name(op_kind, dims):
     buf = ctypes.create_string_buffer(256)
     _check(lib().bh_variant_name(op_kind, arr, buf, 256))
     return buf.value.decode()
+
+
+def tune_cfg_names(op_kind):
+    """Names of the tile configurations the library instantiates for op_kind (0 sgemm, 1 conv)."""
+    out, i = [], 0
+    buf = ctypes.create_string_buffer(64)
+    while lib().bh_tune_cfg_name(op_kind, i, buf, 64) == BH_OK:
+        out.append(buf.value.decode())
+        i += 1
+    return out
 
 
 class DevBuf:
@@ -178,6 +190,9 @@ class Device:
         d = list(dims) + [1] * (4 - len(dims))
         arr = (c_u32 * 4)(*d)
         _check(lib().bh_gen_data(self.ctx, kind, buf.ptr, arr, mode, vi))
+
+    def tune_set(self, op_kind, cfg_index=-1, splits=0):
+        _check(lib().bh_tune_set(self.ctx, op_kind, cfg_index, splits))
 
     def sgemm(self, a, b, c, M, N, K):
         _check(lib().bh_sgemm_kmajor(self.ctx, a.ptr, b.ptr, c.ptr, M, N, K))

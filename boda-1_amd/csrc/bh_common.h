@@ -2,6 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
+#include <dlfcn.h>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "boda_hip.h"
@@ -12,6 +16,13 @@ struct bh_ctx {
   hipDeviceProp_t prop{};
   std::vector<hipEvent_t> events;  // pool; ids index into it
   int events_used = 0;
+  void *ws = nullptr;  // split-K workspace, grown on demand
+  size_t ws_bytes = 0;
+  int ovr_cfg[2] = {-1, -1};  // tuning override per op (0 sgemm, 1 conv); -1 = table/heuristic
+  uint32_t ovr_splits[2] = {0, 0};
+  int ovr_red[2] = {0, 0};
+  void *cnt = nullptr;  // split-K arrival tickets
+  uint64_t cnt_n = 0;
 };
 
 namespace bh {
@@ -56,4 +67,6 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *b
                 uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu);
 std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
 std::string conv_variant(const uint32_t *d);
+int tune_set(bh_ctx *ctx, int op, int cfg, int splits);
+int tune_cfg_name(int op, int cfg, std::string &out);
 }  // namespace bh

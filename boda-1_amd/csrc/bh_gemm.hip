@@ -9,14 +9,21 @@
 // Design (MI355X-first, not a translation of the CUCL register-tile codegen):
 //  * v_mfma_f32_32x32x2_f32: exact fp32 products and accumulation, 64 FLOP/clk/SIMD
 //    = the f32 vector peak, operands one VGPR each (A[i=l&31][k=l>>5], B[k=l>>5][j=l&31]).
-//  * A and B tiles live in LDS as [BK][BM] / [BK][BN] (k-rows). A wave owns a
-//    TM x TN grid of 32x32 MFMA tiles; tile t's row i maps to m = wm0 + TM*i + t,
-//    so one ds_read_b64/b128 returns a lane's operands for all TM (TN) tiles, and
-//    in the epilogue each lane holds TN adjacent output columns (vector stores).
-//  * Global->LDS staging through registers with a double-buffered LDS ring and one
-//    barrier per K-tile; all global reads are buffer loads whose out-of-range /
-//    padding elements are steered to an out-of-bounds offset and come back as 0
-//    (no branches around loads, zero padding for free).
+//    The two lane halves carry different k; we assign half h the k rows
+//    h*BK/2 .. h*BK/2+BK/2-1 of a K tile (any k order is a valid reduction order),
+//    so an m-major A tile is read 4 k at a time with one ds_read_b128.
+//  * LDS tiles: B [BK][BN] (k rows); A [BK][BM] when A is k-major (SGEMM's a),
+//    [BM][BK+4] when A is m-major (conv weights OC x IC*KY*KX), so 8 lanes stream
+//    one 128-B weight row segment with dwordx4 loads. A wave owns a TM x TN grid of
+//    32x32 MFMA tiles; tile t's row i maps to m = wm0 + TM*i + t, so one vector LDS
+//    read returns a lane's operands for all TM (TN) tiles, and in the epilogue each
+//    lane holds TN adjacent output columns (vector stores).
+//  * Register-staged double-buffered LDS ring, one barrier per K tile; every global
+//    read is a buffer load whose out-of-range / padding elements are steered to an
+//    out-of-bounds offset and come back as 0 (no branches around loads).
+//  * Split-K for grids that cannot fill 256 CUs: split s writes raw partial sums to a
+//    workspace slab; a second HBM-bound kernel sums the slabs in fixed order
+//    (bitwise reproducible), adds bias, applies ReLU and scatters to NCHW.
 //  * Block->tile mapping is XCD-aware (bijective remap so blocks sharing an XCD's
 //    L2 get neighbouring tiles) and grouped (8 m-tiles share each B panel).
 //  * The conv B operand is gathered straight from NCHW input (implicit im2col):
@@ -34,15 +41,18 @@ enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
 enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3 };
 
 constexpr uint32_t OOB = 0x80000000u;  // buffer offset that always misses (extents < 2^31)
+constexpr int APAD = 4;                // m-major A tile row padding (floats)
 
 struct GemmArgs {
   const float *a, *b;
   float *c;
   const float *bias;
+  float *ws;       // split-K partial slabs [S][M][ldw]
+  uint32_t *cnt;   // split-K arrival tickets, one per tile (zero between calls)
   uint32_t M, N, K;
-  uint32_t lda, ldb, ldc;
-  uint64_t b_bstride, c_bstride;  // per blockIdx.z, dense B/C only
-  uint32_t a_bytes, b_bytes;      // buffer extents in bytes (reads beyond come back 0)
+  uint32_t lda, ldb, ldc, ldw;
+  uint32_t ks;                // K extent of one split (multiple of BK)
+  uint32_t a_bytes, b_bytes;  // buffer extents in bytes (reads beyond come back 0)
   uint32_t tiles_m, tiles_n;
   int relu;
   int cvec;  // dense C rows can take TN-wide vector stores
@@ -89,18 +99,32 @@ struct fvec<2> { typedef f32x2v t; };
 template <>
 struct fvec<4> { typedef f32x4v t; };
 
-template <int BM, int BN, int BK, int TM, int TN, int WAVES_M, int WAVES_N, int ALD, int BLD>
+template <int N>
+__device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
+  if constexpr (N == 1) return v;
+  else return v[i];
+}
+
+// SPL: 0 = whole K per block; 1 = split-K, partial slabs combined by splitk_reduce_kernel;
+//      2 = split-K, the last-arriving block of a tile combines the slabs in fixed order.
+template <int BM, int BN, int BK, int TM, int TN, int WAVES_M, int WAVES_N, int ALD, int BLD, int SPL>
 __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WAVES_M * WAVES_N * 64;
   constexpr int WM = TM * 32, WN = TN * 32;
   static_assert(BM == WM * WAVES_M && BN == WN * WAVES_N, "tile shape");
-  static_assert(BK % 2 == 0, "BK");
+  static_assert(BK % 8 == 0, "BK must be a multiple of 8");
   constexpr bool IM = (BLD == B_IM2COL || BLD == B_IM1X1);
+  constexpr bool AMM = (ALD == A_MVEC || ALD == A_MSCALAR);  // m-major A tile in LDS
   static_assert(!IM || (NT % BN == 0), "im2col loader needs NT % BN == 0");
+  constexpr int A_LDS = AMM ? BM * (BK + APAD) : BK * BM;  // floats per A buffer
+  constexpr int B_LDS = BK * BN;
+  constexpr int AST = BK + APAD;  // m-major A row stride
 
-  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (BM + BN)];
+  // conv (IM) kernels stage the block's BM biases in LDS behind the tiles
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_LDS + B_LDS) + (IM ? BM : 0)];
   float *const As = smem;
-  float *const Bs = smem + 2 * BK * BM;
+  float *const Bs = smem + 2 * A_LDS;
+  float *const Lbias = smem + 2 * (A_LDS + B_LDS);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -109,10 +133,13 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   uint32_t tile_m, tile_n;
   map_tile(blockIdx.x, p.tiles_m, p.tiles_n, tile_m, tile_n);
   const uint32_t bm0 = tile_m * BM, bn0 = tile_n * BN;
-  const uint32_t z = blockIdx.z;
+  constexpr bool SPLIT = SPL != 0;
+  const uint32_t split = SPLIT ? blockIdx.y : 0;
+  const uint32_t kbeg = split * p.ks;
+  const uint32_t kend = SPLIT ? min(p.K, kbeg + p.ks) : p.K;
 
   const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
-  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(IM ? p.b : p.b + z * p.b_bstride, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
 
   // ---- per-thread constants of the im2col gather (column fixed over the K loop)
   int col_base = 0, iy0 = 0, ix0 = 0;
@@ -159,11 +186,11 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
           const uint32_t m = bm0 + mc, k = k0 + kr;
           sa1[j] = ld1(rsa, (m < p.M && k < p.K) ? (k * p.lda + m) * 4u : OOB);
         } else if constexpr (ALD == A_MVEC) {
-          const int mr = idx % BM, kc = idx / BM;
+          const int kc = idx % (BK / 4), mr = idx / (BK / 4);
           const uint32_t m = bm0 + mr, k = k0 + 4 * kc;
           sa4[j] = ld4(rsa, (m < p.M && k < p.K) ? (m * p.lda + k) * 4u : OOB);
         } else {
-          const int mr = idx % BM, kr = idx / BM;
+          const int kr = idx % BK, mr = idx / BK;
           const uint32_t m = bm0 + mr, k = k0 + kr;
           sa1[j] = ld1(rsa, (m < p.M && k < p.K) ? (m * p.lda + k) * 4u : OOB);
         }
@@ -206,8 +233,8 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   };
 
   auto store_tiles = [&](int buf) {
-    float *const Ab = As + buf * BK * BM;
-    float *const Bb = Bs + buf * BK * BN;
+    float *const Ab = As + buf * A_LDS;
+    float *const Bb = Bs + buf * B_LDS;
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
       const int idx = tid + j * NT;
@@ -219,14 +246,11 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
           const int kr = idx / BM, mc = idx % BM;
           Ab[kr * BM + mc] = sa1[j];
         } else if constexpr (ALD == A_MVEC) {
-          const int mr = idx % BM, kc = idx / BM;
-          Ab[(4 * kc + 0) * BM + mr] = sa4[j][0];
-          Ab[(4 * kc + 1) * BM + mr] = sa4[j][1];
-          Ab[(4 * kc + 2) * BM + mr] = sa4[j][2];
-          Ab[(4 * kc + 3) * BM + mr] = sa4[j][3];
+          const int kc = idx % (BK / 4), mr = idx / (BK / 4);
+          *(f32x4v *)&Ab[mr * AST + 4 * kc] = sa4[j];
         } else {
-          const int mr = idx % BM, kr = idx / BM;
-          Ab[kr * BM + mr] = sa1[j];
+          const int kr = idx % BK, mr = idx / BK;
+          Ab[mr * AST + kr] = sa1[j];
         }
       }
     }
@@ -253,48 +277,120 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
+  const int kh = lane >> 5, li = lane & 31;
   auto compute = [&](int buf) {
-    const float *const Ab = As + buf * BK * BM + wm * WM + TM * (lane & 31);
-    const float *const Bb = Bs + buf * BK * BN + wn * WN + TN * (lane & 31);
-    const int kh = lane >> 5;
+    const float *const Ab = As + buf * A_LDS;
+    const float *const Bb = Bs + buf * B_LDS + wn * WN + TN * li;
 #pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const int kr = 2 * kk + kh;
-      typename fvec<TM>::t av = *(const typename fvec<TM>::t *)&Ab[kr * BM];
-      typename fvec<TN>::t bv = *(const typename fvec<TN>::t *)&Bb[kr * BN];
-      float a[TM], b[TN];
-      if constexpr (TM == 1) a[0] = av; else {
+    for (int kq = 0; kq < BK / 8; ++kq) {
+      f32x4v am[AMM ? TM : 1];
+      if constexpr (AMM) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = av[i];
-      }
-      if constexpr (TN == 1) b[0] = bv; else {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = bv[j];
+        for (int t = 0; t < TM; ++t)
+          am[t] = *(const f32x4v *)&Ab[(wm * WM + TM * li + t) * AST + kh * (BK / 2) + 4 * kq];
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int q = 0; q < 4; ++q) {
+        const int krow = kh * (BK / 2) + 4 * kq + q;
+        float a[TM], b[TN];
+        if constexpr (AMM) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int t = 0; t < TM; ++t) a[t] = am[t][q];
+        } else {
+          typename fvec<TM>::t av = *(const typename fvec<TM>::t *)&Ab[krow * BM + wm * WM + TM * li];
+#pragma unroll
+          for (int t = 0; t < TM; ++t) a[t] = vget<TM>(av, t);
+        }
+        typename fvec<TN>::t bv = *(const typename fvec<TN>::t *)&Bb[krow * BN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = vget<TN>(bv, j);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
     }
   };
 
   // ---- main loop: register-staged, double-buffered LDS, one barrier per K tile
-  const uint32_t nkt = (p.K + BK - 1) / BK;
-  load_tiles(0);
+  const uint32_t nkt = (kend - kbeg + BK - 1) / BK;
+  if constexpr (IM && SPL != 1) {  // rows >= M and a null bias read 0 through the range check
+    const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+    for (int i = tid; i < BM; i += NT) Lbias[i] = ld1(rsbias, bm0 + i < p.M ? (bm0 + i) * 4u : OOB);
+  }
+  load_tiles(kbeg);
   store_tiles(0);
   __syncthreads();
   int buf = 0;
   for (uint32_t kt = 0; kt < nkt; ++kt) {
     const bool more = kt + 1 < nkt;
-    if (more) load_tiles((kt + 1) * BK);
+    if (more) load_tiles(kbeg + (kt + 1) * BK);
     compute(buf);
     if (more) store_tiles(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
 
-  // ---- epilogue: bias, ReLU, stores
-  const uint32_t n_base = bn0 + wn * WN + TN * (lane & 31);
+  // ---- epilogue
+  const uint32_t n_base = bn0 + wn * WN + TN * li;
+  float *const wz = p.ws + (size_t)split * p.M * p.ldw;
+  if constexpr (SPLIT) {
+    // raw partial sums -> slab `split`
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const uint32_t m = bm0 + wm * WM + TM * row + i;
+        if (m >= p.M || n_base >= p.ldw) continue;
+        typename fvec<TN>::t w;
+        if constexpr (TN == 1) w = acc[i][0][r]; else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
+        }
+        *(typename fvec<TN>::t *)&wz[(size_t)m * p.ldw + n_base] = w;
+      }
+    if constexpr (SPL == 1) return;  // bias / ReLU / NCHW scatter happen in splitk_reduce_kernel
+    // Publish the slab and count arrivals (MI355X_MICROARCH.md / cdna_hip_programming.md
+    // G16 split-K recipe): every storing wave drains, barrier, one agent-scope release,
+    // then the ticket. The block drawing S-1 acquires and combines all S slabs.
+    uint32_t *const flag = (uint32_t *)smem;  // tiles are dead after the loop's last barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
+      if (last) {
+        __hip_atomic_store(&p.cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    // fixed order s = 0..S-1 whichever block arrives last (bitwise reproducible)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const uint32_t m = bm0 + wm * WM + TM * row + i;
+        if (m >= p.M || n_base >= p.ldw) continue;
+        float sum[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sum[j] = 0.0f;
+        for (uint32_t q = 0; q < gridDim.y; ++q) {
+          const typename fvec<TN>::t w = *(const typename fvec<TN>::t *)&p.ws[((size_t)q * p.M + m) * p.ldw + n_base];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sum[j] += q == split ? acc[i][j][r] : vget<TN>(w, j);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j][r] = sum[j];
+      }
+  }
   int cofs[TN];
   if constexpr (IM) {
 #pragma unroll
@@ -305,28 +401,27 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
       cofs[j] = col < p.N ? (int)(img * p.OCOHW + pix) : -1;
     }
   }
-  float *const cz = IM ? p.c : p.c + z * p.c_bstride;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
       const uint32_t m = bm0 + wm * WM + TM * row + i;
       if (m >= p.M) continue;
       float v[TN];
-      const float bv = p.bias ? p.bias[m] : 0.0f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        float x = acc[i][j][r] + bv;
+        float x = acc[i][j][r];
+        if constexpr (IM) x += Lbias[wm * WM + TM * row + i];
         v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
       }
       if constexpr (IM) {
-        float *const crow = cz + (size_t)m * p.OHW;
+        float *const crow = p.c + (size_t)m * p.OHW;
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           if (cofs[j] >= 0) crow[cofs[j]] = v[j];
       } else {
-        float *const crow = cz + (size_t)m * p.ldc + n_base;
+        float *const crow = p.c + (size_t)m * p.ldc + n_base;
         if (p.cvec && n_base + TN <= p.N) {
           typename fvec<TN>::t w;
           if constexpr (TN == 1) w = v[0]; else {
@@ -344,29 +439,93 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   }
 }
 
+// Split-K combine: out = act(bias + sum_s ws[s]) in fixed s order (deterministic).
+// HBM-bound; consecutive threads walk consecutive columns of one row.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p, uint32_t S, int im) {
+  const uint64_t total = (uint64_t)p.M * p.N;
+  const uint64_t slab = (uint64_t)p.M * p.ldw;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = (uint32_t)(e / p.N), n = (uint32_t)(e - (uint64_t)m * p.N);
+    const float *w = p.ws + (size_t)m * p.ldw + n;
+    float s = 0.0f;
+    for (uint32_t i = 0; i < S; ++i) s += w[i * slab];
+    if (p.bias) s += p.bias[m];
+    if (p.relu && s < 0.0f) s = 0.0f;
+    if (im) {
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+      const uint32_t pix = n - img * p.OHW;
+      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + pix] = s;
+    } else {
+      p.c[(size_t)m * p.ldc + n] = s;
+    }
+  }
+}
+
+
 // ---------------------------------------------------------------------------
-// host side: tile configurations and dispatch
+// host side: tile-configuration table, split-K planning, tuning table, dispatch
 // ---------------------------------------------------------------------------
 
-struct TileCfg {
-  int BM, BN, BK, TM, TN, WAVES_M, WAVES_N;
+typedef void (*kern_t)(GemmArgs);
+
+struct cfg_t {
   const char *name;
+  int BM, BN, BK, NT;
+  kern_t k[4][4][3];  // [A loader][B loader][SPL]
 };
 
-// Instantiated configurations (name used for reporting / wisdom).
-#define CFG_L 128, 128, 16, 2, 2, 2, 2  // 4 waves, 64x64 per wave
-#define CFG_M 64, 128, 16, 1, 2, 2, 2   // 4 waves, 32x64 per wave (OC <= 64)
-#define CFG_S 32, 256, 16, 1, 2, 1, 4   // 4 waves, 32x64 per wave (OC <= 32)
-
 template <int BM, int BN, int BK, int TM, int TN, int WM_, int WN_, int ALD, int BLD>
-int launch_cfg(bh_ctx *ctx, GemmArgs &p, uint32_t batch, const char *what) {
-  p.tiles_m = (p.M + BM - 1) / BM;
-  p.tiles_n = (p.N + BN - 1) / BN;
-  const uint64_t nblk = (uint64_t)p.tiles_m * p.tiles_n;
-  if (nblk > 0x7fffffffu || batch > 65535) return bh::fail(BH_UNSUP, std::string(what) + ": grid too large");
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD>), dim3((uint32_t)nblk, 1, batch),
-                     dim3(WM_ * WN_ * 64), 0, ctx->stream, p);
-  return bh::check_launch(what);
+void reg_kernels(cfg_t &c) {
+  c.k[ALD][BLD][0] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 0>;
+  c.k[ALD][BLD][1] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 1>;
+  c.k[ALD][BLD][2] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 2>;
+}
+template <int BM, int BN, int BK, int TM, int TN, int WM_, int WN_>
+cfg_t conv_cfg(const char *name) {
+  cfg_t c{name, BM, BN, BK, WM_ * WN_ * 64, {}};
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_MVEC, B_IM2COL>(c);
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_MSCALAR, B_IM2COL>(c);
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_MVEC, B_IM1X1>(c);
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_MSCALAR, B_IM1X1>(c);
+  return c;
+}
+template <int BM, int BN, int BK, int TM, int TN, int WM_, int WN_>
+cfg_t sgemm_cfg(const char *name) {
+  cfg_t c{name, BM, BN, BK, WM_ * WN_ * 64, {}};
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_KVEC, B_KVEC>(c);
+  reg_kernels<BM, BN, BK, TM, TN, WM_, WN_, A_KSCALAR, B_KSCALAR>(c);
+  return c;
+}
+
+// Tile configurations (BM x BN x BK; 32x32 MFMA tiles per wave TM x TN; waves M x N).
+const std::vector<cfg_t> &cfgs(int op) {
+  static const std::vector<cfg_t> sg = {
+      sgemm_cfg<128, 128, 16, 2, 2, 2, 2>("128x128x16"),
+      sgemm_cfg<128, 128, 32, 2, 2, 2, 2>("128x128x32"),
+      sgemm_cfg<256, 128, 16, 4, 2, 2, 2>("256x128x16"),
+      sgemm_cfg<128, 64, 16, 2, 1, 2, 2>("128x64x16"),
+      sgemm_cfg<64, 64, 16, 1, 1, 2, 2>("64x64x16"),
+  };
+  static const std::vector<cfg_t> cv = {
+      conv_cfg<128, 128, 32, 2, 2, 2, 2>("128x128x32"),
+      conv_cfg<128, 128, 16, 2, 2, 2, 2>("128x128x16"),
+      conv_cfg<64, 128, 32, 1, 2, 2, 2>("64x128x32"),
+      conv_cfg<32, 256, 32, 1, 2, 1, 4>("32x256x32"),
+      conv_cfg<64, 64, 32, 1, 1, 2, 2>("64x64x32"),
+      conv_cfg<128, 64, 32, 2, 1, 2, 2>("128x64x32"),
+      conv_cfg<128, 32, 32, 1, 1, 4, 1>("128x32x32"),
+      conv_cfg<256, 128, 16, 4, 2, 2, 2>("256x128x16"),
+      conv_cfg<64, 32, 32, 1, 1, 2, 1>("64x32x32"),
+  };
+  return op == 0 ? sg : cv;
+}
+
+int cfg_index(int op, std::string const &name) {
+  auto const &v = cfgs(op);
+  for (size_t i = 0; i < v.size(); ++i)
+    if (name == v[i].name) return (int)i;
+  return -1;
 }
 
 bool fits_buffer(uint64_t bytes) { return bytes < (uint64_t)OOB - 64; }
@@ -377,14 +536,230 @@ void set_fd(uint32_t d, uint32_t &m, uint32_t &s) {
   s = f.s;
 }
 
+int ensure_ws(bh_ctx *ctx, size_t bytes) {
+  if (ctx->ws_bytes >= bytes) return BH_OK;
+  if (ctx->ws) {
+    BH_HIP(hipStreamSynchronize(ctx->stream));
+    BH_HIP(hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+  }
+  size_t want = bytes + (bytes >> 2);
+  BH_HIP(hipMalloc(&ctx->ws, want));
+  ctx->ws_bytes = want;
+  return BH_OK;
+}
+
+// split-K arrival tickets: zeroed once at allocation, reset by each tile's last arriver
+int ensure_cnt(bh_ctx *ctx, uint64_t n) {
+  if (ctx->cnt_n >= n) return BH_OK;
+  if (ctx->cnt) {
+    BH_HIP(hipStreamSynchronize(ctx->stream));
+    BH_HIP(hipFree(ctx->cnt));
+    ctx->cnt = nullptr;
+    ctx->cnt_n = 0;
+  }
+  uint64_t want = std::max<uint64_t>(n, 4096);
+  BH_HIP(hipMalloc(&ctx->cnt, want * 4));
+  BH_HIP(hipMemsetAsync(ctx->cnt, 0, want * 4, ctx->stream));
+  ctx->cnt_n = want;
+  return BH_OK;
+}
+
+// Number of K splits: enough blocks to cover the CUs twice, at least MIN_KT K tiles per split.
+uint32_t plan_splits(uint32_t tiles, uint32_t K, int BK, uint32_t ncu) {
+  const uint32_t MIN_KT = 4;
+  const uint32_t nkt = (K + BK - 1) / BK;
+  if (tiles >= ncu || nkt < 2 * MIN_KT) return 1;
+  uint32_t s = (2 * ncu + tiles - 1) / tiles;
+  s = std::min(s, nkt / MIN_KT);
+  s = std::min(s, 64u);
+  return std::max(s, 1u);
+}
+
+// ---- tuning table ("wisdom" for this backend): exact-shape -> (config, splits)
+struct choice_t {
+  int cfg = -1;
+  uint32_t splits = 0;  // 0 = plan
+  int red = 0;          // split-K combine: 0 = plan, 1 = reduce kernel, 2 = in-kernel last arriver
+};
+std::map<std::string, choice_t> g_tune;
+std::once_flag g_tune_once;
+
+std::string shape_key(int op, const uint32_t *d) {
+  std::string k = op == 0 ? "sgemm" : "conv";
+  int n = op == 0 ? 3 : 11;
+  for (int i = 0; i < n; ++i) k += " " + std::to_string(d[i]);
+  return k;
+}
+
+void load_tuning() {
+  std::string path;
+  if (const char *e = getenv("BH_TUNE_FILE")) path = e;
+  else {
+    Dl_info info;
+    if (dladdr((void *)&load_tuning, &info) && info.dli_fname) {
+      std::string so = info.dli_fname;
+      size_t sl = so.rfind('/');
+      path = (sl == std::string::npos ? std::string(".") : so.substr(0, sl)) + "/../tuning/gfx950.tune";
+    }
+  }
+  FILE *f = path.empty() ? nullptr : fopen(path.c_str(), "r");
+  if (!f) return;
+  char line[512];
+  while (fgets(line, sizeof(line), f)) {
+    // "<op> d0 d1 ... cfg=<name> splits=<n>"
+    std::string l(line);
+    if (l.empty() || l[0] == '#') continue;
+    size_t c = l.find(" cfg="), s = l.find(" splits=");
+    if (c == std::string::npos || s == std::string::npos) continue;
+    std::string key = l.substr(0, c);
+    std::string name = l.substr(c + 5, s - c - 5);
+    int op = key.rfind("sgemm", 0) == 0 ? 0 : 1;
+    choice_t ch;
+    ch.cfg = cfg_index(op, name);
+    ch.splits = (uint32_t)strtoul(l.c_str() + s + 8, nullptr, 10);
+    size_t r = l.find(" red=");
+    if (r != std::string::npos) ch.red = l[r + 5] == 'k' ? 1 : 2;
+    if (ch.cfg >= 0) g_tune[key] = ch;
+  }
+  fclose(f);
+}
+
+choice_t heuristic(int op, const uint32_t *d) {
+  choice_t ch;
+  if (op == 0) {
+    ch.cfg = 0;
+    return ch;
+  }
+  uint32_t B = d[0], H = d[2], W = d[3], OC = d[4], KY = d[5], KX = d[6], sy = d[7], sx = d[8], py = d[9], px = d[10];
+  uint64_t N = (uint64_t)B * ((H + 2 * py - KY) / sy + 1) * ((W + 2 * px - KX) / sx + 1);
+  const char *n = "128x128x32";
+  if (N <= 32) n = "128x32x32";
+  else if (N <= 64) n = "128x64x32";
+  else if (OC <= 32) n = "32x256x32";
+  else if (OC <= 64) n = "64x128x32";
+  ch.cfg = cfg_index(1, n);
+  return ch;
+}
+
+choice_t choose(bh_ctx *ctx, int op, const uint32_t *d) {
+  if (ctx && ctx->ovr_cfg[op] >= 0) {
+    choice_t ch;
+    ch.cfg = ctx->ovr_cfg[op];
+    ch.splits = ctx->ovr_splits[op];
+    ch.red = ctx->ovr_red[op];
+    return ch;
+  }
+  std::call_once(g_tune_once, load_tuning);
+  auto it = g_tune.find(shape_key(op, d));
+  if (it != g_tune.end()) return it->second;
+  return heuristic(op, d);
+}
+
+uint32_t resolve_splits(cfg_t const &c, choice_t const &ch, uint32_t M, uint32_t N, uint32_t K, uint32_t ncu) {
+  uint32_t tiles = ((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
+  uint32_t nkt = (K + c.BK - 1) / c.BK;
+  uint32_t S = ch.splits ? ch.splits : plan_splits(tiles, K, c.BK, ncu);
+  S = std::max(1u, std::min(S, nkt));
+  uint32_t ks = ((nkt + S - 1) / S) * c.BK;
+  return (K + ks - 1) / ks;  // splits actually used (none empty)
+}
+
+int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmArgs &p, const char *what) {
+  cfg_t const &c = cfgs(op)[ch.cfg];
+  p.tiles_m = (p.M + c.BM - 1) / c.BM;
+  p.tiles_n = (p.N + c.BN - 1) / c.BN;
+  const uint64_t nblk = (uint64_t)p.tiles_m * p.tiles_n;
+  if (nblk > 0x7fffffffu) return bh::fail(BH_UNSUP, std::string(what) + ": grid too large");
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  const uint32_t S = resolve_splits(c, ch, p.M, p.N, p.K, ncu);
+  const uint32_t nkt = (p.K + c.BK - 1) / c.BK;
+  p.ks = ((nkt + S - 1) / S) * c.BK;
+  // in-kernel combine unless asked otherwise or the tile grid is large (then a separate,
+  // fully parallel reduce pass is cheaper than serial combining by last arrivers)
+  const int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 && S > 8 ? 1 : 2));
+  kern_t k = c.k[ald][bld][red];
+  if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
+  void *args[] = {&p};
+  if (S > 1) {
+    p.ldw = (p.N + 3) & ~3u;
+    int rc = ensure_ws(ctx, (size_t)S * p.M * p.ldw * 4);
+    if (rc != BH_OK) return rc;
+    p.ws = (float *)ctx->ws;
+    if (red == 2) {
+      rc = ensure_cnt(ctx, nblk);
+      if (rc != BH_OK) return rc;
+      p.cnt = (uint32_t *)ctx->cnt;
+      BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, 0, ctx->stream));
+      return bh::check_launch(what);
+    }
+    BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, 0, ctx->stream));
+    const uint64_t total = (uint64_t)p.M * p.N;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
+    const int im = (bld == B_IM2COL || bld == B_IM1X1) ? 1 : 0;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, ctx->stream, p, S, im);
+    return bh::check_launch("splitk_reduce");
+  }
+  BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, 1, 1), dim3(c.NT), args, 0, ctx->stream));
+  return bh::check_launch(what);
+}
+
+void conv_dims(const uint32_t *d, uint32_t &M, uint32_t &N, uint32_t &K) {
+  uint32_t B = d[0], IC = d[1], H = d[2], W = d[3], OC = d[4], KY = d[5], KX = d[6], sy = d[7], sx = d[8],
+           py = d[9], px = d[10];
+  M = OC;
+  N = B * ((H + 2 * py - KY) / sy + 1) * ((W + 2 * px - KX) / sx + 1);
+  K = IC * KY * KX;
+}
+
+std::string describe(int op, const uint32_t *d, choice_t const &ch) {
+  cfg_t const &c = cfgs(op)[ch.cfg];
+  uint32_t M, N, K;
+  std::string s;
+  if (op == 0) {
+    M = d[0]; N = d[1]; K = d[2];
+    s = std::string("mfma32_sgemm_") + c.name + ((M % 4 == 0 && N % 4 == 0) ? "_vec" : "_scalar");
+  } else {
+    conv_dims(d, M, N, K);
+    bool k1 = d[5] == 1 && d[6] == 1 && d[7] == 1 && d[8] == 1 && d[9] == 0 && d[10] == 0;
+    s = std::string("mfma32_conv_") + (k1 ? "1x1_" : "im2col_") + c.name + ((K % 4 == 0) ? "_avec" : "_ascalar");
+  }
+  uint32_t S = resolve_splits(c, ch, M, N, K, 256);
+  if (S > 1) {
+    uint64_t nblk = (uint64_t)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
+    int red = ch.red ? ch.red : (nblk >= 64 && S > 8 ? 1 : 2);
+    s += "_splitk" + std::to_string(S) + (red == 1 ? "k" : "i");
+  }
+  return s;
+}
+
 }  // namespace
 
 namespace bh {
 
 std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K) {
-  (void)K;
-  bool vec = (M % 4 == 0) && (N % 4 == 0);
-  return std::string("mfma32_sgemm_128x128x16") + (vec ? "_vec" : "_scalar");
+  uint32_t d[3] = {M, N, K};
+  return describe(0, d, choose(nullptr, 0, d));
+}
+
+std::string conv_variant(const uint32_t *d) { return describe(1, d, choose(nullptr, 1, d)); }
+
+int tune_set(bh_ctx *ctx, int op, int cfg, int splits) {
+  if (op < 0 || op > 1) return fail(BH_ERR, "tune_set: op must be 0 (sgemm) or 1 (conv)");
+  if (cfg >= (int)cfgs(op).size()) return fail(BH_UNSUP, "tune_set: no such config");
+  ctx->ovr_cfg[op] = cfg < 0 ? -1 : cfg;
+  // splits: 0 = planned; n > 0 = n splits, combined in-kernel; -n = n splits, reduce kernel
+  ctx->ovr_splits[op] = splits > 0 ? (uint32_t)splits : (uint32_t)(-splits);
+  ctx->ovr_red[op] = splits > 0 ? 2 : (splits < 0 ? 1 : 0);
+  return BH_OK;
+}
+
+int tune_cfg_name(int op, int cfg, std::string &out) {
+  if (op < 0 || op > 1) return fail(BH_ERR, "op must be 0 (sgemm) or 1 (conv)");
+  if (cfg < 0 || cfg >= (int)cfgs(op).size()) return fail(BH_UNSUP, "no such config");
+  out = cfgs(op)[cfg].name;
+  return BH_OK;
 }
 
 int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t M, uint32_t N, uint32_t K) {
@@ -398,26 +773,10 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
   p.b_bytes = (uint32_t)((uint64_t)K * N * 4);
   p.relu = 0;
   const bool vec = (M % 4 == 0) && (N % 4 == 0) && ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0);
-  p.cvec = (N % 2 == 0) && ((uintptr_t)c % 8 == 0);
-  if (vec) return launch_cfg<CFG_L, A_KVEC, B_KVEC>(ctx, p, 1, "sgemm");
-  return launch_cfg<CFG_L, A_KSCALAR, B_KSCALAR>(ctx, p, 1, "sgemm");
-}
-
-namespace {
-struct conv_shape {
-  uint32_t B, IC, H, W, OC, KY, KX, sy, sx, py, px, OH, OW;
-};
-int pick_tile(uint32_t OC) { return OC <= 32 ? 2 : (OC <= 64 ? 1 : 0); }
-}  // namespace
-
-std::string conv_variant(const uint32_t *d) {
-  uint32_t IC = d[1], OC = d[4], KY = d[5], KX = d[6], sy = d[7], sx = d[8], py = d[9], px = d[10];
-  bool k1 = KY == 1 && KX == 1 && sy == 1 && sx == 1 && py == 0 && px == 0;
-  uint32_t K = IC * KY * KX;
-  static const char *tiles[3] = {"128x128x16", "64x128x16", "32x256x16"};
-  std::string s = std::string("mfma32_conv_") + (k1 ? "1x1_" : "im2col_") + tiles[pick_tile(OC)];
-  s += (K % 4 == 0) ? "_avec" : "_ascalar";
-  return s;
+  p.cvec = (N % 4 == 0) && ((uintptr_t)c % 16 == 0);
+  uint32_t d[3] = {M, N, K};
+  choice_t ch = choose(ctx, 0, d);
+  return launch_gemm(ctx, 0, ch, vec ? A_KVEC : A_KSCALAR, vec ? B_KVEC : B_KSCALAR, p, "sgemm");
 }
 
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *biases, float *out, uint32_t B,
@@ -446,20 +805,9 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *b
   set_fd(OW, p.ow_m, p.ow_s);
   const bool k1 = KY == 1 && KX == 1 && sy == 1 && sx == 1 && py == 0 && px == 0;
   const bool avec = (K % 4 == 0) && ((uintptr_t)filts % 16 == 0);
-  const int t = pick_tile(OC);
-#define DISPATCH(CFG)                                                                              \
-  do {                                                                                             \
-    if (k1) {                                                                                      \
-      if (avec) return launch_cfg<CFG, A_MVEC, B_IM1X1>(ctx, p, 1, "conv");                        \
-      return launch_cfg<CFG, A_MSCALAR, B_IM1X1>(ctx, p, 1, "conv");                               \
-    }                                                                                              \
-    if (avec) return launch_cfg<CFG, A_MVEC, B_IM2COL>(ctx, p, 1, "conv");                         \
-    return launch_cfg<CFG, A_MSCALAR, B_IM2COL>(ctx, p, 1, "conv");                                \
-  } while (0)
-  if (t == 0) DISPATCH(CFG_L);
-  if (t == 1) DISPATCH(CFG_M);
-  DISPATCH(CFG_S);
-#undef DISPATCH
+  uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
+  choice_t ch = choose(ctx, 1, d);
+  return launch_gemm(ctx, 1, ch, avec ? A_MVEC : A_MSCALAR, k1 ? B_IM1X1 : B_IM2COL, p, "conv");
 }
 
 }  // namespace bh

@@ -73,6 +73,8 @@ int bh_destroy(bh_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->cnt) (void)hipFree(c->cnt);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return BH_OK;
@@ -81,7 +83,7 @@ int bh_destroy(bh_ctx *c) {
 int bh_plat_tag(bh_ctx *c, char *buf, size_t n) {
   BH_CHECK_CTX(c);
   if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
-  std::snprintf(buf, n, "hip:%s:%s", c->prop.name, c->prop.gcnArchName);
+  std::snprintf(buf, n, "hip:%s:%s", c->prop.name[0] ? c->prop.name : "MI355X", c->prop.gcnArchName);
   return BH_OK;
 }
 
@@ -204,6 +206,19 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
   else return bh::fail(BH_ERR, "unknown op kind");
   std::snprintf(buf, n, "%s", s.c_str());
   return BH_OK;
+}
+
+int bh_tune_set(bh_ctx *c, int op, int cfg_index, int splits) {
+  BH_CHECK_CTX(c);
+  return bh::tune_set(c, op, cfg_index, splits);
+}
+
+int bh_tune_cfg_name(int op, int cfg_index, char *buf, size_t n) {
+  if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
+  std::string s;
+  int rc = bh::tune_cfg_name(op, cfg_index, s);
+  if (rc == BH_OK) std::snprintf(buf, n, "%s", s.c_str());
+  return rc;
 }
 
 }  // extern "C"

@@ -1,0 +1,205 @@
+// hip_compute.cc -- hip_compute_t : rtc_compute_t, Boda's be=hip backend over
+// libboda_hip.so (include/boda_hip.h).
+//
+// Contract followed (nvrtc_compute_t, src/nvrtc_util.cc:174-395):
+//   * vars are device buffers keyed by name, zero-filled at creation (:80-84);
+//     reshaped views share the buffer (src/rtc_compute.cc:29-41);
+//   * run() brackets each call with a begin/end event pair and returns a call id;
+//     get_dur(b,e) is begin(b) -> end(e) in milliseconds (:289-298, :367-381);
+//   * the hot ops are hand-written kernels reached by function name, the way
+//     the reference reaches cuBLAS/cuDNN through its culibs intercept
+//     (src/nvrtc_util.cc:369-372): hip_sgemm, hip_conv, and the gen_data_*
+//     test-pattern generators. Generic CUCL source is not JIT-compiled by this
+//     backend: compile() rejects it with unsup_err, which ops-prof records
+//     and skips (src/rtc_prof.cc:287-296).
+#include <cstring>
+#include <memory>
+
+#include "boda_hip.h"
+#include "op_desc.H"
+#include "rtc_compute.H"
+
+namespace boda_hip {
+
+void rtc_launch_check_blks_and_tpb(std::string const &name, uint64_t blks, uint64_t tpb) {
+  if (!blks || !tpb) rt_err("rtc launch of '" + name + "' with zero blks or tpb");
+}
+
+namespace {
+
+void bh_check(int rc, std::string const &what) {
+  if (rc == BH_OK) return;
+  std::string m = what + ": " + bh_last_error();
+  if (rc == BH_UNSUP) unsup_err(m);
+  rt_err(m);
+}
+
+struct var_info_t {
+  std::shared_ptr<void> buf;  // device memory, shared by reshaped views
+  dims_t dims;
+};
+
+struct call_ev_t {
+  int b, e;
+};
+
+struct hip_compute_t : public rtc_compute_t {
+  int device;
+  bh_ctx *ctx = nullptr;
+  std::map<std::string, var_info_t> vars;
+  std::map<std::string, rtc_func_info_t> funcs;
+  std::vector<call_ev_t> calls;
+
+  explicit hip_compute_t(int dev) : device(dev) {}
+  ~hip_compute_t() override {
+    vars.clear();
+    if (ctx) bh_destroy(ctx);
+  }
+
+  void init() override { bh_check(bh_init(device, &ctx), "bh_init"); }
+
+  std::string get_plat_tag() override {
+    char buf[256];
+    bh_check(bh_plat_tag(ctx, buf, sizeof(buf)), "bh_plat_tag");
+    return buf;
+  }
+
+  var_info_t &must_var(std::string const &vn) {
+    auto it = vars.find(vn);
+    if (it == vars.end()) rt_err("hip_compute: no var named '" + vn + "'");
+    return it->second;
+  }
+
+  void create_var_with_dims(std::string const &vn, dims_t const &dims) override {
+    if (vars.count(vn)) rt_err("hip_compute: var '" + vn + "' exists");
+    void *p = nullptr;
+    bh_check(bh_alloc(ctx, dims.bytes(), &p), "bh_alloc(" + vn + ")");
+    bh_ctx *c = ctx;
+    vars[vn] = var_info_t{std::shared_ptr<void>(p, [c](void *q) { bh_free(c, q); }), dims};
+  }
+
+  void create_var_with_dims_as_reshaped_view_of_var(std::string const &vn, dims_t const &dims,
+                                                    std::string const &src_vn) override {
+    var_info_t &s = must_var(src_vn);
+    if (s.dims.tn != dims.tn || s.dims.elems() != dims.elems())
+      rt_err("reshape of '" + src_vn + "' to '" + vn + "' changes type or element count");
+    vars[vn] = var_info_t{s.buf, dims};
+  }
+
+  void release_var(std::string const &vn) override {
+    must_var(vn);
+    bh_check(bh_sync(ctx), "bh_sync");
+    vars.erase(vn);
+  }
+  dims_t get_var_dims(std::string const &vn) override { return must_var(vn).dims; }
+  void set_var_to_zero(std::string const &vn) override {
+    var_info_t &v = must_var(vn);
+    bh_check(bh_memset0(ctx, v.buf.get(), v.dims.bytes()), "bh_memset0");
+  }
+
+  void compile(std::vector<rtc_func_info_t> const &fis, rtc_compile_opts_t const &) override {
+    for (auto const &fi : fis) {
+      bool known = fi.func_name == "hip_sgemm" || fi.func_name == "hip_conv" ||
+                   fi.func_name.rfind("gen_data_", 0) == 0;
+      if (!known)
+        unsup_err("be=hip runs the hand-written gfx950 kernels (hip_sgemm, hip_conv, gen_data_*); '" +
+                  fi.func_name + "' would need CUCL JIT, which this backend does not provide");
+      funcs[fi.func_name] = fi;
+    }
+  }
+  void release_func(std::string const &fn) override { funcs.erase(fn); }
+  void release_all_funcs() override { funcs.clear(); }
+
+  float *arg_ptr(rtc_func_call_t const &rfc, std::string const &an, bool optional = false) {
+    auto it = rfc.arg_map.find(an);
+    if (it == rfc.arg_map.end()) {
+      if (optional) return nullptr;
+      rt_err("call of '" + rfc.rtc_func_name + "' lacks arg '" + an + "'");
+    }
+    return (float *)must_var(it->second.n).buf.get();
+  }
+  double arg_val(rtc_func_call_t const &rfc, std::string const &an, double dflt) {
+    auto it = rfc.arg_map.find(an);
+    return (it == rfc.arg_map.end() || !it->second.has_v) ? dflt : it->second.v;
+  }
+  dims_t const &arg_dims(rtc_func_call_t const &rfc, std::string const &an) {
+    auto it = rfc.arg_map.find(an);
+    if (it == rfc.arg_map.end()) rt_err("call of '" + rfc.rtc_func_name + "' lacks arg '" + an + "'");
+    return must_var(it->second.n).dims;
+  }
+
+  uint32_t run(rtc_func_call_t const &rfc) override {
+    auto fit = funcs.find(rfc.rtc_func_name);
+    if (fit == funcs.end()) rt_err("hip_compute: function '" + rfc.rtc_func_name + "' not compiled");
+    rtc_func_info_t const &fi = fit->second;
+    call_ev_t ev{};
+    bh_check(bh_event_record(ctx, &ev.b), "bh_event_record");
+    std::string const &fn = fi.func_name;
+    if (fn == "hip_sgemm") {
+      dims_t const &a = arg_dims(rfc, "a"), &b = arg_dims(rfc, "b");
+      uint32_t M = a.dsz("M"), K = a.dsz("K"), N = b.dsz("N");
+      if (b.dsz("K") != K) rt_err("hip_sgemm: a/b K mismatch");
+      bh_check(bh_sgemm_kmajor(ctx, arg_ptr(rfc, "a"), arg_ptr(rfc, "b"), arg_ptr(rfc, "c"), M, N, K), "hip_sgemm");
+    } else if (fn == "hip_conv") {
+      conv_shape_t s = get_conv_shape(fi.op);
+      auto r = fi.op.scalars.find("conv_has_relu");
+      int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
+      bh_check(bh_conv2d_fwd_nchw(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "biases", true),
+                                  arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py,
+                                  s.px, relu),
+               "hip_conv");
+    } else {  // gen_data_<type>_<arg>
+      std::string an = fn.substr(fn.rfind('_') + 1);
+      uint32_t mode = (uint32_t)arg_val(rfc, "mode", 5);
+      float vi = (float)arg_val(rfc, "vi", 0.0);
+      dims_t const &d = arg_dims(rfc, an);
+      uint32_t dd[4] = {1, 1, 1, 1};
+      int kind;
+      if (fn == "gen_data_sgemm_a") kind = BH_GEN_SGEMM_A;
+      else if (fn == "gen_data_sgemm_b") kind = BH_GEN_SGEMM_B;
+      else if (fn == "gen_data_Convolution_in") kind = BH_GEN_CONV_IN;
+      else if (fn == "gen_data_Convolution_filts") kind = BH_GEN_CONV_FILTS;
+      else if (fn == "gen_data_Convolution_biases") kind = BH_GEN_CONV_BIASES;
+      else unsup_err("no gen_data generator '" + fn + "'");
+      if (d.d.size() > 4) rt_err("gen_data: too many dims");
+      for (size_t i = 0; i < d.d.size(); ++i) dd[i] = d.d[i].sz;
+      bh_check(bh_gen_data(ctx, kind, arg_ptr(rfc, an), dd, mode, vi), fn);
+    }
+    bh_check(bh_event_record(ctx, &ev.e), "bh_event_record");
+    calls.push_back(ev);
+    return (uint32_t)(calls.size() - 1);
+  }
+
+  void finish_and_sync() override { bh_check(bh_sync(ctx), "bh_sync"); }
+  void release_per_call_id_data() override {
+    calls.clear();
+    bh_check(bh_events_reset(ctx), "bh_events_reset");
+  }
+  float get_dur(uint32_t const &b, uint32_t const &e) override {
+    if (b >= calls.size() || e >= calls.size()) rt_err("get_dur: bad call id");
+    float ms = 0;
+    bh_check(bh_elapsed_ms(ctx, calls[b].b, calls[e].e, &ms), "bh_elapsed_ms");
+    return ms;
+  }
+  void profile_start() override {}
+  void profile_stop() override {}
+
+  void copy_var_to_nda(p_nda_t const &nda, std::string const &vn) override {
+    var_info_t &v = must_var(vn);
+    if (nda->dims.elems() != v.dims.elems()) rt_err("copy_var_to_nda: size mismatch for '" + vn + "'");
+    if (!nda->data) nda->data = std::make_shared<std::vector<float>>(v.dims.elems());
+    bh_check(bh_d2h(ctx, nda->elems(), v.buf.get(), v.dims.bytes()), "bh_d2h");
+  }
+  void *get_var_raw_native_pointer(std::string const &vn) override { return must_var(vn).buf.get(); }
+  void copy_nda_to_var(std::string const &vn, p_nda_t const &nda) override {
+    var_info_t &v = must_var(vn);
+    if (nda->dims.elems() != v.dims.elems()) rt_err("copy_nda_to_var: size mismatch for '" + vn + "'");
+    bh_check(bh_h2d(ctx, v.buf.get(), nda->elems(), v.dims.bytes()), "bh_h2d");
+  }
+};
+
+}  // namespace
+
+p_rtc_compute_t make_hip_compute(int device) { return std::make_shared<hip_compute_t>(device); }
+
+}  // namespace boda_hip

@@ -1,0 +1,293 @@
+// ops_prof.cc -- boda_hip_ops_prof: Boda's per-op profiling sweep (ops-prof,
+// src/rtc_prof.cc:139-371 with profile_rcg_call :44-126) over be=hip.
+//
+// For each op of an op list (either dialect): annotate it for the hip backend,
+// create its vars (zero-filled), fill the inputs with gen_data on the device,
+// run the main kernel --run-iter times, take the event-timed duration of the
+// last call, digest every output (seed = std::hash of the var name) and compare
+// it with the known-good digest of --wisdom-in-fn using the reference's own
+// mrd_comp, write --wisdom-out-fn (kg digests, and runs with --write-runs=1) and
+// print ***ALL IS WELL*** or ***MAD FAILS***, as the reference does.
+// --shard=k/n runs only the ops a greedy LPT partition (by roofline time) gives
+// to shard k of n, so n processes (one per GPU, --device=k) split a list with no
+// communication at all.
+// --selftest-wisdom=F needs no GPU: decodes every kg digest of F, re-encodes it and
+// checks the hex round-trips byte-identically and the sample plan matches.
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+
+#include "nda_digest.H"
+#include "op_desc.H"
+#include "rtc_compute.H"
+
+using namespace boda_hip;
+
+namespace {
+
+struct opts_t {
+  std::map<std::string, std::string> kv;
+  std::string get(std::string const &k, std::string const &d = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : it->second;
+  }
+};
+
+int selftest_wisdom(std::string const &fn) {
+  std::ifstream in(fn);
+  if (!in) rt_err("cannot open " + fn);
+  std::string line, prev;
+  size_t n = 0;
+  while (std::getline(in, line)) {
+    if (prev == "kg") {
+      std::string vn = line, hex;
+      std::getline(in, hex);
+      nda_digest_t d = nda_digest_t::from_hex(hex);
+      if (d.to_hex() != hex) rt_err("hex round trip differs for a digest of " + vn);
+      if (d.plan().size() != d.samps.size()) rt_err("sample plan size differs for a digest of " + vn);
+      ++n;
+      line.clear();
+    }
+    prev = line;
+  }
+  std::ifstream in2(fn);
+  op_wisdom_t w;
+  size_t nops = 0;
+  while (read_next_wisdom(in2, w)) {
+    parse_op_line(w.op_line);
+    ++nops;
+  }
+  std::cout << "selftest ok: " << n << " digests, " << nops << " op_wisdom blocks\n";
+  return 0;
+}
+
+// structural op equality, as the reference's op_base_t comparison (src/rtc_prof.cc:238)
+bool same_op(op_base_t const &a, op_base_t const &b) {
+  if (a.type != b.type || a.str_vals != b.str_vals || a.scalars != b.scalars) return false;
+  if (a.dims_vals.size() != b.dims_vals.size()) return false;
+  for (auto const &kv : a.dims_vals) {
+    auto it = b.dims_vals.find(kv.first);
+    if (it == b.dims_vals.end() || it->second != kv.second) return false;
+  }
+  return true;
+}
+
+std::vector<std::string> arg_vars(op_base_t const &op) {
+  if (op.type == "Convolution") return {"in", "filts", "biases", "out"};
+  return {"a", "b", "c"};
+}
+std::vector<std::string> in_vars(op_base_t const &op) {
+  if (op.type == "Convolution") return {"in", "filts", "biases"};
+  return {"a", "b"};
+}
+std::vector<std::string> out_vars(op_base_t const &op) {
+  if (op.type == "Convolution") return {"out"};
+  return {"c"};
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  opts_t o;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a.rfind("--", 0) != 0) {
+      std::cerr << "bad argument " << a << "\n";
+      return 2;
+    }
+    size_t eq = a.find('=');
+    o.kv[a.substr(2, eq == std::string::npos ? std::string::npos : eq - 2)] =
+        eq == std::string::npos ? "1" : a.substr(eq + 1);
+  }
+  try {
+    if (o.kv.count("selftest-wisdom")) return selftest_wisdom(o.get("selftest-wisdom"));
+    if (o.kv.count("dump-ops")) {  // parse-only: one line per Convolution/sgemm op, no GPU needed
+      size_t skipped = 0;
+      for (auto const &op : read_op_list(o.get("dump-ops"), &skipped)) {
+        op_work_t w = op_work(op);
+        if (op.type == "Convolution") {
+          conv_shape_t s = get_conv_shape(op);
+          std::printf("Convolution %u %u %u %u %u %u %u %u %u %u %u %.0f %.0f\n", s.B, s.IC, s.H, s.W, s.OC, s.KY,
+                      s.KX, s.sy, s.sx, s.py, s.px, w.flops, w.bytes);
+        } else {
+          sgemm_shape_t s = get_sgemm_shape(op);
+          std::printf("sgemm %u %u %u %.0f %.0f\n", s.M, s.N, s.K, w.flops, w.bytes);
+        }
+      }
+      std::printf("skipped %zu\n", skipped);
+      return 0;
+    }
+    std::string ops_fn = o.get("ops-fn");
+    if (ops_fn.empty()) {
+      std::cerr << "usage: boda_hip_ops_prof --ops-fn=F [--wisdom-in-fn=F] [--wisdom-out-fn=F] [--out-fn=F]\n"
+                   "  [--gen-data-mode=5] [--run-iter=1] [--mrd-toler=2e-4] [--device=0] [--write-runs=0]\n"
+                   "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F\n";
+      return 2;
+    }
+    const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
+    const uint32_t run_iter = std::max(1ul, std::stoul(o.get("run-iter", "1")));
+    const double mrd = std::stod(o.get("mrd-toler", "2e-4"));
+    const bool write_runs = o.get("write-runs", "0") != "0";
+    uint32_t skip = std::stoul(o.get("skip-ops", "0"));
+    std::ofstream fout;
+    std::ostream *out = &std::cout;
+    if (!o.get("out-fn").empty()) {
+      fout.open(o.get("out-fn"));
+      out = &fout;
+    }
+    std::ifstream win;
+    if (!o.get("wisdom-in-fn").empty()) {
+      win.open(o.get("wisdom-in-fn"));
+      if (!win) rt_err("cannot open wisdom-in " + o.get("wisdom-in-fn"));
+    }
+    std::ofstream wout;
+    if (!o.get("wisdom-out-fn").empty()) wout.open(o.get("wisdom-out-fn"));
+
+    // every line of the list (the wisdom file has one block per line, whatever the type)
+    std::vector<std::string> lines;
+    {
+      std::ifstream f(ops_fn);
+      if (!f) rt_err("cannot open " + ops_fn);
+      std::string l;
+      while (std::getline(f, l))
+        if (!l.empty()) lines.push_back(l);
+    }
+    // optional LPT shard by roofline time
+    std::vector<bool> mine(lines.size(), true);
+    std::string shard = o.get("shard");
+    if (!shard.empty()) {
+      uint32_t k = std::stoul(shard.substr(0, shard.find('/'))), n = std::stoul(shard.substr(shard.find('/') + 1));
+      std::vector<std::pair<double, size_t>> cost;
+      for (size_t i = 0; i < lines.size(); ++i) {
+        op_base_t op = parse_op_line(lines[i]);
+        double c = (op.type == "Convolution" || op.type == "sgemm") ? roofline_secs(op_work(op)) : 0.0;
+        cost.emplace_back(c, i);
+      }
+      std::stable_sort(cost.begin(), cost.end(), [](auto const &x, auto const &y) { return x.first > y.first; });
+      std::vector<double> load(n, 0.0);
+      for (auto const &c : cost) {
+        size_t j = std::min_element(load.begin(), load.end()) - load.begin();
+        load[j] += c.first;
+        mine[c.second] = (j == k);
+      }
+    }
+
+    p_rtc_compute_t rtc = make_hip_compute(std::stoi(o.get("device", "0")));
+    rtc->init();
+    const std::string plat = rtc->get_plat_tag();
+    const std::string tune = "(use_be=hip)";
+    uint32_t num_fail = 0, n_run = 0;
+    double sum_flops = 0, sum_secs = 0, sum_roof = 0;
+    for (size_t ix = 0; ix < lines.size(); ++ix) {
+      op_wisdom_t wi;
+      bool have_wi = win.is_open() && read_next_wisdom(win, wi);
+      if (skip) {
+        --skip;
+        continue;
+      }
+      op_base_t op = parse_op_line(lines[ix]);
+      if (have_wi && !same_op(parse_op_line(wi.op_line), op)) rt_err("op mismatch between input wisdom and ops-list at op " + std::to_string(ix));
+      if (!mine[ix]) continue;
+      op_wisdom_t wo;
+      wo.op_line = lines[ix];
+      op_run_t run;
+      run.plat_tag = plat;
+      std::ostringstream err, err_extra;
+      std::map<std::string, p_nda_t> outs;
+      try {
+        add_hip_annotations(op);
+        std::vector<rtc_func_info_t> fis{{op.func_name, "", {}, op}};
+        for (auto const &vn : in_vars(op)) fis.push_back({"gen_data_" + op.type + "_" + vn, "", {}, op});
+        rtc->compile(fis, rtc_compile_opts_t());
+        for (auto const &vn : arg_vars(op)) rtc->create_var_with_dims(vn, op.get_dims(vn));
+        for (auto const &vn : in_vars(op)) {
+          rtc_func_call_t g;
+          g.rtc_func_name = "gen_data_" + op.type + "_" + vn;
+          g.arg_map[vn] = vn;
+          g.arg_map["mode"] = rtc_arg_t::val(mode);
+          g.arg_map["vi"] = rtc_arg_t::val(0.0);
+          rtc->run(g);
+        }
+        rtc_func_call_t c;
+        c.rtc_func_name = op.func_name;
+        for (auto const &vn : arg_vars(op)) c.arg_map[vn] = vn;
+        uint32_t call_id = 0;
+        for (uint32_t r = 0; r < run_iter; ++r) call_id = rtc->run(c);
+        rtc->finish_and_sync();
+        run.rt_secs = rtc->get_dur(call_id, call_id) / 1000.0;
+        for (auto const &vn : out_vars(op)) outs[vn] = rtc->create_nda_from_var(vn);
+        run.op_line = op.line;
+      } catch (unsup_exception const &e) {
+        err << "profile call failure: " << e.what();
+      }
+      for (auto const &vn : arg_vars(op))
+        if (op.has_dims(vn)) {
+          try {
+            rtc->release_var(vn);
+          } catch (rt_exception const &) {
+          }
+        }
+      rtc->release_per_call_id_data();
+      rtc->release_all_funcs();
+      std::string dstat = "n/a";
+      if (err.str().empty()) {
+        for (auto const &kv : outs) {
+          nda_digest_t d = nda_digest_t::make(kv.second->elems(), kv.second->dims, digest_seed_for(kv.first));
+          wo.kgs.emplace_back(kv.first, d);
+          if (have_wi) {
+            dstat = "ok";
+            for (auto const &kg : wi.kgs)
+              if (kg.first == kv.first) {
+                double worst = 0;
+                std::string cr = kg.second.mrd_comp(d, mrd, &worst);
+                if (!cr.empty()) {
+                  dstat = "FAIL";
+                  err << kv.first << " digest mrd_comp() failure vs stored digest (worst rd/tol "
+                      << worst << ")";
+                  err_extra << "comp_res:\n" << cr;
+                }
+              }
+          }
+        }
+        op_work_t w = op_work(op);
+        sum_flops += w.flops;
+        sum_secs += run.rt_secs;
+        sum_roof += roofline_secs(w);
+        ++n_run;
+        char buf[512];
+        std::snprintf(buf, sizeof(buf), "op_ix=%zu func=%s secs=%.6e gflops=%.1f roofline=%.1f%% digest=%s\n", ix,
+                      op.func_name.c_str(), run.rt_secs, w.flops / run.rt_secs / 1e9,
+                      100.0 * roofline_secs(w) / run.rt_secs, dstat.c_str());
+        *out << buf;
+      }
+      run.err = err.str();
+      if (!run.err.empty()) {
+        ++num_fail;
+        *out << "-----\n errors for op_ix=" << ix << " op='" << lines[ix] << "'\n--  comp fail for op_tune='" << tune
+             << "'\n" << run.err << "\n" << err_extra.str();
+      }
+      if (wout.is_open()) {
+        if (write_runs) wo.tunes.push_back({tune, {run}});
+        write_wisdom(wout, wo);
+        wout.flush();
+      }
+      out->flush();
+    }
+    if (n_run) {
+      char buf[256];
+      std::snprintf(buf, sizeof(buf), "summary: ops=%u sum_gflop=%.3f sum_kernel_ms=%.4f agg_gflops=%.1f roofline_frac=%.4f plat=%s\n",
+                    n_run, sum_flops / 1e9, sum_secs * 1e3, sum_flops / sum_secs / 1e9, sum_roof / sum_secs,
+                    plat.c_str());
+      *out << buf;
+    }
+    if (!num_fail) *out << "***ALL IS WELL***\n";
+    else *out << "***MAD FAILS*** num_mad_fail=" << num_fail << "\n";
+    return num_fail ? 1 : 0;
+  } catch (rt_exception const &e) {
+    std::cerr << "error: " << e.what() << "\n";
+    return 3;
+  }
+}

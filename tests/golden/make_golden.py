@@ -110,6 +110,9 @@ def main():
         with open(os.path.join(HERE, s + ".json"), "w") as f:
             json.dump(ents, f, separators=(",", ":"))
         print(s, len(ents), "ops")
+    os.makedirs(os.path.join(HERE, "wis"), exist_ok=True)
+    for s in SUITES:  # the original text files too, for the C++ wisdom reader's round-trip test
+        shutil.copyfile(os.path.join(REF, "test/good_tr", s, "wisdom.wis"), os.path.join(HERE, "wis", s + ".wis"))
     os.makedirs(os.path.join(HERE, "ops"), exist_ok=True)
     for o in OP_LISTS:
         shutil.copyfile(os.path.join(REF, "test", o), os.path.join(HERE, "ops", o))

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Sweep tile configurations x K-splits per op on the GPU and write the tuning table.
+
+The backend's counterpart of Boda's op_tune sweeps + wisdom (src/rtc_prof.cc
+ops-prof over several --op-tunes; src/op-tuner.cc): for every op of the given
+op lists, time each instantiated tile configuration with each split count
+(median of --reps event-timed launches after a warm-up), keep the fastest and
+write boda-1_amd/tuning/gfx950.tune lines "<op> <dims> cfg=<name> splits=<n>".
+Results of every candidate go to --json for analysis.
+
+  python tools/tune.py --sets conv,sgemm-full --out boda-1_amd/tuning/gfx950.tune
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "boda-1_amd"))
+sys.path.insert(0, ROOT)
+
+import boda_hip  # noqa: E402
+from boda_hip import ops, runner  # noqa: E402
+
+SETS = {"sgemm-full": "sgemm-ops-full.txt", "sgemm-small": "sgemm-ops-small.txt",
+        "conv": "conv-ops-1-5-20-nin-alex-gn.txt", "op-sigs": "op_sigs_full.txt"}
+SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
+CFG_BK = {}
+
+
+def bk_of(name):
+    return int(name.split("x")[2])
+
+
+def time_op(dev, wl, i, reps):
+    wl.launch(i)  # warm-up (also grows the split-K workspace)
+    ts = []
+    for _ in range(reps):
+        b = dev.event()
+        wl.launch(i)
+        e = dev.event()
+        ts.append((b, e))
+    dev.sync()
+    out = [dev.elapsed_ms(b, e) for b, e in ts]
+    dev.events_reset()
+    return statistics.median(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sets", default="conv,sgemm-full,sgemm-small")
+    ap.add_argument("--out", default=os.path.join(ROOT, "boda-1_amd", "tuning", "gfx950.tune"))
+    ap.add_argument("--json", default="")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--max-flop-sgemm", type=float, default=3e12, help="skip sgemm sweeps above this (use heuristic)")
+    args = ap.parse_args()
+
+    dev = boda_hip.Device(0)
+    plat = dev.plat_tag()
+    names = {0: boda_hip.tune_cfg_names(0), 1: boda_hip.tune_cfg_names(1)}
+    table, results = {}, []
+    t_start = time.time()
+    for sname in args.sets.split(","):
+        o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", SETS[sname]))
+        shapes = []
+        for op in o:
+            s = ops.shape_of(op)
+            if s not in shapes:
+                shapes.append(s)
+        for s in shapes:
+            kind = 0 if isinstance(s, ops.SgemmShape) else 1
+            dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
+            key = ("sgemm " if kind == 0 else "conv ") + " ".join(map(str, dims))
+            if key in table:
+                continue
+            wl = runner.Workload(dev, [s])
+            M, N, K = (s.M, s.N, s.K) if kind == 0 else (s.OC, s.B * s.OH * s.OW, s.K)
+            dev.tune_set(kind, -1, 0)
+            t_def = time_op(dev, wl, 0, args.reps)
+            best = (t_def, -1, 0)
+            cand = []
+            if not (kind == 0 and s.flops() > args.max_flop_sgemm):
+                for ci, cn in enumerate(names[kind]):
+                    nkt = -(-K // bk_of(cn))
+                    for S in SPLITS:
+                        if S > 1 and nkt < 2 * S:
+                            continue
+                        cand.append((ci, S))
+                        if S > 1:
+                            cand.append((ci, -S))  # same split, separate reduce kernel
+            for ci, S in cand:
+                dev.tune_set(kind, ci, S)
+                try:
+                    t = time_op(dev, wl, 0, args.reps)
+                except boda_hip.UnsupportedError:
+                    continue
+                results.append({"key": key, "cfg": names[kind][ci], "splits": S, "ms": t})
+                if t < best[0]:
+                    best = (t, ci, S)
+            dev.tune_set(kind, -1, 0)
+            wl.free()
+            results.append({"key": key, "cfg": "default", "splits": 0, "ms": t_def})
+            if best[1] >= 0:
+                table[key] = (names[kind][best[1]], best[2], best[0], t_def)
+            rf = runner.roofline_secs(s) * 1e3
+            print("%-48s default %.4f ms  best %s S=%+d %.4f ms  roofline %.4f ms (%.0f%%)" % (
+                key, t_def, names[kind][best[1]] if best[1] >= 0 else "default", best[2], best[0], rf,
+                100 * rf / best[0]), flush=True)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        f.write("# boda-1_amd tuning table (tools/tune.py) for %s; <op> <dims> cfg=<tile config> splits=<K splits>\n"
+                % plat)
+        for k, (cn, S, t, td) in table.items():
+            f.write("%s cfg=%s splits=%d red=%s\n" % (k, cn, abs(S), "k" if S < 0 else "i"))
+    if args.json:
+        json.dump({"plat": plat, "results": results}, open(args.json, "w"))
+    print("wrote %d entries to %s in %.0f s" % (len(table), args.out, time.time() - t_start))
+    dev.close()
+
+
+if __name__ == "__main__":
+    main()
