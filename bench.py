@@ -11,8 +11,11 @@ device with the reference's gen_data mode 5 before the timed region).
   per_set     = per op-list aggregate in the reference's own convention:
                 sum flops / sum event-timed kernel seconds (src/rtc_prof.cc:104-124),
                 plus sum(roofline time) / sum(kernel time)
-  roofline    = the dominant kernel (most event time): algorithmic flops per launch
-                / its average launch duration (HIP events on its stream), vs fp32 peak
+  launch      = each timed step is a captured hipGraph (no host launch latency
+                between ops; --eager for op-by-op launches from Python)
+  roofline    = the dominant kernel (most time): algorithmic flops per launch / its
+                average launch duration measured on its stream (device timestamps
+                between ops inside the replayed graph), vs fp32 peak
   cpu_baseline= the oracle's fp32 OpenMP CPU implementation (kind "port") on a
                 bounded sample, rank 0 at N=1 only
 
@@ -142,6 +145,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--per-op", default="", help="write per-op event times (JSON) to this path")
+    ap.add_argument("--eager", action="store_true", help="launch op by op from Python instead of hipGraph replay")
     args = ap.parse_args()
 
     dd = Dist()
@@ -163,23 +167,39 @@ def main():
         wl.step()
     dev.sync()
 
-    events = []
+    # one captured hipGraph per timed step, with a device timestamp between ops
+    # (--eager: launch op by op from Python, timed with HIP event pairs)
+    nop = len(my_shapes)
+    graphs, events = [], []
+    if not args.eager:
+        for k in range(args.steps):
+            graphs.append(wl.capture_step(stamp_base=k * (nop + 1)))
     dd.barrier()
     dev.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step(events)
+    if args.eager:
+        for _ in range(args.steps):
+            wl.step(events)
+    else:
+        for g in graphs:
+            dev.graph_launch(g)
     dev.sync()
     t1 = time.perf_counter()
     dd.barrier()
     elapsed = dd.max(t1 - t0)
 
-    # per-op kernel times (events on the context's stream), mean over the timed steps
-    ktime = [0.0] * len(my_shapes)
-    for i, b, e in events:
-        ktime[i] += dev.elapsed_ms(b, e) / 1e3
+    # per-op kernel times on the context's stream, mean over the timed steps
+    ktime = [0.0] * nop
+    if args.eager:
+        for i, b, e in events:
+            ktime[i] += dev.elapsed_ms(b, e) / 1e3
+        dev.events_reset()
+    else:
+        ts = dev.stamps_read(0, args.steps * (nop + 1))
+        for k in range(args.steps):
+            for i in range(nop):
+                ktime[i] += (ts[k * (nop + 1) + i + 1] - ts[k * (nop + 1) + i]) / 1e6
     ktime = [t / args.steps for t in ktime]
-    dev.events_reset()
 
     my_flops = sum(s.flops() for s in my_shapes)
     total_flops = dd.sum(my_flops) * args.steps
@@ -245,6 +265,9 @@ def main():
             "scaling": "strong" if (args.strong and dd.world > 1) else "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (reference gen_data mode 5, generated on device)",
             "config": {"workload": " + ".join(SETS[n] for n in set_names) + " (one main-kernel launch per op per step)",
+                       "launch": "eager" if args.eager else "hipGraph replay of each step",
+                       "op_timing": "HIP event pair per op" if args.eager else
+                       "device wall-clock stamp between ops inside the graph (op + one stamp + seams)",
                        "ops_per_gpu": len(my_shapes), "gflop_per_step_per_gpu": round(my_flops / 1e9, 3),
                        "parallelism": ("op-shard" if args.strong else "op-replica") + "%d" % dd.world,
                        "plat": dev.plat_tag()},
@@ -253,6 +276,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    for g in graphs:
+        dev.graph_destroy(g)
     wl.free()
     dev.close()
     dd.close()

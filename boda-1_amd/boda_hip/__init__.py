@@ -22,7 +22,9 @@ GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5
 EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_destroy", "bh_plat_tag",
            "bh_get_stream", "bh_alloc", "bh_free", "bh_memset0", "bh_h2d", "bh_d2h", "bh_sync",
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
-           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name"]
+           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
+           "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
+           "bh_stamp", "bh_stamps_read"]
 
 
 class BodaHipError(RuntimeError):
@@ -67,6 +69,12 @@ def lib():
         L.bh_sgemm_kmajor.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32]
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
+        L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
+        L.bh_stamps_read.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        L.bh_capture_begin.argtypes = [c_vp]
+        L.bh_capture_end.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int)]
+        L.bh_graph_launch.argtypes = [c_vp, ctypes.c_int]
+        L.bh_graph_destroy.argtypes = [c_vp, ctypes.c_int]
         L.bh_tune_set.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.bh_tune_cfg_name.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
         _lib = L
@@ -190,6 +198,29 @@ class Device:
         d = list(dims) + [1] * (4 - len(dims))
         arr = (c_u32 * 4)(*d)
         _check(lib().bh_gen_data(self.ctx, kind, buf.ptr, arr, mode, vi))
+
+    def stamp(self, slot):
+        _check(lib().bh_stamp(self.ctx, slot))
+
+    def stamps_read(self, first, n):
+        """Slots first..first+n-1 in microseconds relative to slot first (syncs)."""
+        out = (ctypes.c_double * n)()
+        _check(lib().bh_stamps_read(self.ctx, first, n, out))
+        return list(out)
+
+    def capture_begin(self):
+        _check(lib().bh_capture_begin(self.ctx))
+
+    def capture_end(self):
+        g = ctypes.c_int(-1)
+        _check(lib().bh_capture_end(self.ctx, ctypes.byref(g)))
+        return g.value
+
+    def graph_launch(self, g):
+        _check(lib().bh_graph_launch(self.ctx, g))
+
+    def graph_destroy(self, g):
+        _check(lib().bh_graph_destroy(self.ctx, g))
 
     def tune_set(self, op_kind, cfg_index=-1, splits=0):
         _check(lib().bh_tune_set(self.ctx, op_kind, cfg_index, splits))

@@ -5,7 +5,9 @@ For each op: create its vars on the device (zero-filled), fill the inputs with
 the reference's gen_data (mode 5 by default) on the device, then launch the
 main kernel as often as asked, timing each launch between a pair of HIP
 events on the context's stream (the reference times exactly this: one
-main-kernel call, no data generation or layout transforms, F7).
+main-kernel call, no data generation or layout transforms, F7). A step can be
+captured into a hipGraph and replayed, so the GPU runs the op sweep back to
+back instead of waiting on per-launch host latency.
 """
 from dataclasses import dataclass
 
@@ -72,10 +74,14 @@ class Workload:
     def output(self, i):
         return self.ops[i].bufs[-1].download()
 
-    def step(self, timed_events=None):
+    def step(self, timed_events=None, stamp_base=None):
         """One pass over every op (one main-kernel launch each). With timed_events (a list),
-        appends (op index, begin event, end event)."""
+        appends (op index, begin event, end event). With stamp_base, writes a device
+        timestamp into slot stamp_base + i before op i and one after the last op, so op i
+        took stamps[i+1] - stamps[i] (its kernel(s) plus one stamp and the launch seams)."""
         for i in range(len(self.ops)):
+            if stamp_base is not None:
+                self.dev.stamp(stamp_base + i)
             if timed_events is not None:
                 b = self.dev.event()
                 self.launch(i)
@@ -83,6 +89,18 @@ class Workload:
                 timed_events.append((i, b, e))
             else:
                 self.launch(i)
+        if stamp_base is not None:
+            self.dev.stamp(stamp_base + len(self.ops))
+
+    def capture_step(self, stamp_base=None):
+        """Capture one step into a hipGraph (HIP events cannot be timed inside graphs,
+        so per-op times come from device stamps, see step()). Returns the graph id."""
+        self.dev.capture_begin()
+        try:
+            self.step(stamp_base=stamp_base)
+        finally:
+            g = self.dev.capture_end()
+        return g
 
     def free(self):
         for v in self.ops:

@@ -21,6 +21,9 @@ struct bh_ctx {
   int ovr_cfg[2] = {-1, -1};  // tuning override per op (0 sgemm, 1 conv); -1 = table/heuristic
   uint32_t ovr_splits[2] = {0, 0};
   int ovr_red[2] = {0, 0};
+  std::vector<hipGraphExec_t> graphs;  // captured launch sequences
+  void *stamps = nullptr;              // device timestamp slots (bh_stamp)
+  double stamp_hz = 100e6;
   void *cnt = nullptr;  // split-K arrival tickets
   uint64_t cnt_n = 0;
 };

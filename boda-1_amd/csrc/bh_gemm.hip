@@ -47,10 +47,11 @@ struct GemmArgs {
   const float *a, *b;
   float *c;
   const float *bias;
-  float *ws;       // split-K partial slabs [S][M][ldw]
+  float *ws;       // split-K partial slabs, tile-major: [S][tile][BM*BN]
   uint32_t *cnt;   // split-K arrival tickets, one per tile (zero between calls)
   uint32_t M, N, K;
-  uint32_t lda, ldb, ldc, ldw;
+  uint32_t lda, ldb, ldc;
+  uint32_t tbm, tbn;          // tile shape (for the split-K combine)
   uint32_t ks;                // K extent of one split (multiple of BK)
   uint32_t a_bytes, b_bytes;  // buffer extents in bytes (reads beyond come back 0)
   uint32_t tiles_m, tiles_n;
@@ -103,6 +104,42 @@ template <int N>
 __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
   if constexpr (N == 1) return v;
   else return v[i];
+}
+
+// Split-K combine of one float4 chunk of one tile: sum the S partial slabs in fixed
+// order s = 0..S-1 (bitwise reproducible whoever combines), add bias, ReLU, store
+// to the dense C or scatter to NCHW. Used by the reduce kernel and by the last-
+// arriving block of a tile. chunk c covers tile elements 4c..4c+3 (row-major BM x BN).
+template <int IMODE>
+__device__ __forceinline__ void combine_store(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
+                                              uint32_t c, uint32_t S, const float *bias_lds) {
+  const size_t tsz = (size_t)p.tbm * p.tbn, slab = tsz * p.tiles_m * p.tiles_n;
+  const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
+  f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t q = 0;
+  for (; q + 4 <= S; q += 4) {  // four slabs in flight
+    f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
+    f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
+    sum += a0; sum += a1; sum += a2; sum += a3;
+  }
+  for (; q < S; ++q) sum += src[q * slab / 4];
+  const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
+  const uint32_t m = tile_m * p.tbm + row;
+  if (m >= p.M) return;
+  const float b = bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t n = tile_n * p.tbn + col0 + t;
+    if (n >= p.N) break;
+    float x = sum[t] + b;
+    if (p.relu && x < 0.0f) x = 0.0f;
+    if constexpr (IMODE) {
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW)] = x;
+    } else {
+      p.c[(size_t)m * p.ldc + n] = x;
+    }
+  }
 }
 
 // SPL: 0 = whole K per block; 1 = split-K, partial slabs combined by splitk_reduce_kernel;
@@ -333,37 +370,36 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
 
   // ---- epilogue
   const uint32_t n_base = bn0 + wn * WN + TN * li;
-  float *const wz = p.ws + (size_t)split * p.M * p.ldw;
   if constexpr (SPLIT) {
-    // raw partial sums -> slab `split`
+    // raw partial sums -> this split's slab of this tile (tile-major, row-major BM x BN)
+    const uint32_t tile = tile_m * p.tiles_n + tile_n;
+    float *const wz = p.ws + ((size_t)split * p.tiles_m * p.tiles_n + tile) * (BM * BN);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const uint32_t m = bm0 + wm * WM + TM * row + i;
-        if (m >= p.M || n_base >= p.ldw) continue;
+        const int row = wm * WM + TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
         typename fvec<TN>::t w;
         if constexpr (TN == 1) w = acc[i][0][r]; else {
 #pragma unroll
           for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
         }
-        *(typename fvec<TN>::t *)&wz[(size_t)m * p.ldw + n_base] = w;
+        *(typename fvec<TN>::t *)&wz[row * BN + wn * WN + TN * li] = w;
       }
     if constexpr (SPL == 1) return;  // bias / ReLU / NCHW scatter happen in splitk_reduce_kernel
-    // Publish the slab and count arrivals (MI355X_MICROARCH.md / cdna_hip_programming.md
-    // G16 split-K recipe): every storing wave drains, barrier, one agent-scope release,
-    // then the ticket. The block drawing S-1 acquires and combines all S slabs.
-    uint32_t *const flag = (uint32_t *)smem;  // tiles are dead after the loop's last barrier
+    // Publish the slab and count arrivals (cdna_hip_programming.md split-K recipe):
+    // every storing wave drains, barrier, one agent-scope release, then the ticket.
+    // The block drawing S-1 acquires and combines all S slabs of the tile.
+    uint32_t *const flag = (uint32_t *)smem;  // the A/B tiles are dead after the loop's last barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
       if (last) {
-        __hip_atomic_store(&p.cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
+        __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -371,25 +407,9 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
     }
     __syncthreads();
     if (!*flag) return;
-    // fixed order s = 0..S-1 whichever block arrives last (bitwise reproducible)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const uint32_t m = bm0 + wm * WM + TM * row + i;
-        if (m >= p.M || n_base >= p.ldw) continue;
-        float sum[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) sum[j] = 0.0f;
-        for (uint32_t q = 0; q < gridDim.y; ++q) {
-          const typename fvec<TN>::t w = *(const typename fvec<TN>::t *)&p.ws[((size_t)q * p.M + m) * p.ldw + n_base];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) sum[j] += q == split ? acc[i][j][r] : vget<TN>(w, j);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j][r] = sum[j];
-      }
+    for (uint32_t c = tid; c < BM * BN / 4; c += NT)
+      combine_store<IM ? 1 : 0>(p, tile, tile_m, tile_n, c, gridDim.y, IM ? Lbias : nullptr);
+    return;
   }
   int cofs[TN];
   if constexpr (IM) {
@@ -439,29 +459,17 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   }
 }
 
-// Split-K combine: out = act(bias + sum_s ws[s]) in fixed s order (deterministic).
-// HBM-bound; consecutive threads walk consecutive columns of one row.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p, uint32_t S, int im) {
-  const uint64_t total = (uint64_t)p.M * p.N;
-  const uint64_t slab = (uint64_t)p.M * p.ldw;
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t m = (uint32_t)(e / p.N), n = (uint32_t)(e - (uint64_t)m * p.N);
-    const float *w = p.ws + (size_t)m * p.ldw + n;
-    float s = 0.0f;
-    for (uint32_t i = 0; i < S; ++i) s += w[i * slab];
-    if (p.bias) s += p.bias[m];
-    if (p.relu && s < 0.0f) s = 0.0f;
-    if (im) {
-      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
-      const uint32_t pix = n - img * p.OHW;
-      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + pix] = s;
-    } else {
-      p.c[(size_t)m * p.ldc + n] = s;
-    }
+// Split-K combine pass (SPL == 1): one thread per float4 chunk of every tile.
+template <int IMODE>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p, uint32_t S) {
+  const uint32_t per_tile = p.tbm * p.tbn / 4, ntiles = p.tiles_m * p.tiles_n;
+  const uint64_t total = (uint64_t)per_tile * ntiles;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t tile = (uint32_t)(e / per_tile), c = (uint32_t)(e - (uint64_t)tile * per_tile);
+    const uint32_t tile_m = tile / p.tiles_n, tile_n = tile - tile_m * p.tiles_n;
+    combine_store<IMODE>(p, tile, tile_m, tile_n, c, S, nullptr);
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // host side: tile-configuration table, split-K planning, tuning table, dispatch
@@ -634,12 +642,17 @@ choice_t heuristic(int op, const uint32_t *d) {
   }
   uint32_t B = d[0], H = d[2], W = d[3], OC = d[4], KY = d[5], KX = d[6], sy = d[7], sx = d[8], py = d[9], px = d[10];
   uint64_t N = (uint64_t)B * ((H + 2 * py - KY) / sy + 1) * ((W + 2 * px - KX) / sx + 1);
+  uint32_t K = d[1] * KY * KX;
+  // big grids: 128x128 tiles; grids that cannot fill the GPU: narrow tiles plus
+  // split-K combined by the reduce kernel (the tuning table refines both)
   const char *n = "128x128x32";
+  uint64_t tiles128 = ((OC + 127) / 128) * ((N + 127) / 128);
   if (N <= 32) n = "128x32x32";
-  else if (N <= 64) n = "128x64x32";
   else if (OC <= 32) n = "32x256x32";
   else if (OC <= 64) n = "64x128x32";
+  else if (tiles128 < 256 && K >= 256) n = "128x32x32";
   ch.cfg = cfg_index(1, n);
+  ch.red = 1;
   return ch;
 }
 
@@ -678,13 +691,14 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   p.ks = ((nkt + S - 1) / S) * c.BK;
   // in-kernel combine unless asked otherwise or the tile grid is large (then a separate,
   // fully parallel reduce pass is cheaper than serial combining by last arrivers)
-  const int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 && S > 8 ? 1 : 2));
+  const int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2));
   kern_t k = c.k[ald][bld][red];
   if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
   void *args[] = {&p};
   if (S > 1) {
-    p.ldw = (p.N + 3) & ~3u;
-    int rc = ensure_ws(ctx, (size_t)S * p.M * p.ldw * 4);
+    p.tbm = c.BM;
+    p.tbn = c.BN;
+    int rc = ensure_ws(ctx, (size_t)S * nblk * c.BM * c.BN * 4);
     if (rc != BH_OK) return rc;
     p.ws = (float *)ctx->ws;
     if (red == 2) {
@@ -695,10 +709,12 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
       return bh::check_launch(what);
     }
     BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, 0, ctx->stream));
-    const uint64_t total = (uint64_t)p.M * p.N;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
-    const int im = (bld == B_IM2COL || bld == B_IM1X1) ? 1 : 0;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, ctx->stream, p, S, im);
+    const uint64_t total = nblk * c.BM * c.BN / 4;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
+    if (bld == B_IM2COL || bld == B_IM1X1)
+      hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3(grid), dim3(256), 0, ctx->stream, p, S);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<0>, dim3(grid), dim3(256), 0, ctx->stream, p, S);
     return bh::check_launch("splitk_reduce");
   }
   BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, 1, 1), dim3(c.NT), args, 0, ctx->stream));
@@ -728,7 +744,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
   uint32_t S = resolve_splits(c, ch, M, N, K, 256);
   if (S > 1) {
     uint64_t nblk = (uint64_t)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
-    int red = ch.red ? ch.red : (nblk >= 64 && S > 8 ? 1 : 2);
+    int red = ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2);
     s += "_splitk" + std::to_string(S) + (red == 1 ? "k" : "i");
   }
   return s;

@@ -13,6 +13,13 @@
 
 namespace {
 thread_local std::string g_last_error;
+
+// Device timestamp: one lane writes the constant-rate wall clock (s_memrealtime).
+// Usable inside captured graphs, where HIP event timing is not available.
+__global__ void stamp_kernel(unsigned long long *t, int slot) {
+  if (threadIdx.x == 0) t[slot] = wall_clock64();
+}
+constexpr int STAMP_SLOTS = 1 << 18;
 }
 
 namespace bh {
@@ -60,6 +67,12 @@ int bh_init(int device, bh_ctx **out) {
     return bh::fail(BH_ERR, "device is " + arch + "; libboda_hip is built for gfx950 (MI355X) only");
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->stamps, STAMP_SLOTS * sizeof(unsigned long long));
+  if (e == hipSuccess) {
+    int khz = 0;
+    e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+    c->stamp_hz = khz > 0 ? khz * 1000.0 : 100e6;
+  }
   if (e != hipSuccess) {
     delete c;
     return bh::fail(BH_ERR, std::string("bh_init: ") + hipGetErrorString(e));
@@ -73,7 +86,10 @@ int bh_destroy(bh_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
+  for (hipGraphExec_t g : c->graphs)
+    if (g) (void)hipGraphExecDestroy(g);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->stamps) (void)hipFree(c->stamps);
   if (c->cnt) (void)hipFree(c->cnt);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -205,6 +221,60 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
   else if (op == 1) s = bh::conv_variant(dims);
   else return bh::fail(BH_ERR, "unknown op kind");
   std::snprintf(buf, n, "%s", s.c_str());
+  return BH_OK;
+}
+
+int bh_stamp(bh_ctx *c, int slot) {
+  BH_CHECK_CTX(c);
+  if (slot < 0 || slot >= STAMP_SLOTS) return bh::fail(BH_ERR, "stamp slot out of range");
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, c->stream, (unsigned long long *)c->stamps, slot);
+  return bh::check_launch("stamp");
+}
+
+int bh_stamps_read(bh_ctx *c, int first, int n, double *us) {
+  BH_CHECK_CTX(c);
+  if (!us || first < 0 || n < 0 || first + n > STAMP_SLOTS) return bh::fail(BH_ERR, "bad stamp range");
+  std::vector<unsigned long long> t(n);
+  BH_HIP(hipMemcpyAsync(t.data(), (unsigned long long *)c->stamps + first, n * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, c->stream));
+  BH_HIP(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < n; ++i) us[i] = (double)(t[i] - t[0]) * 1e6 / c->stamp_hz;
+  return BH_OK;
+}
+
+int bh_capture_begin(bh_ctx *c) {
+  BH_CHECK_CTX(c);
+  BH_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  return BH_OK;
+}
+
+int bh_capture_end(bh_ctx *c, int *graph_id) {
+  BH_CHECK_CTX(c);
+  if (!graph_id) return bh::fail(BH_ERR, "null out");
+  hipGraph_t g = nullptr;
+  BH_HIP(hipStreamEndCapture(c->stream, &g));
+  hipGraphExec_t ge = nullptr;
+  hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return bh::fail(BH_ERR, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  c->graphs.push_back(ge);
+  *graph_id = (int)c->graphs.size() - 1;
+  return BH_OK;
+}
+
+int bh_graph_launch(bh_ctx *c, int graph_id) {
+  BH_CHECK_CTX(c);
+  if (graph_id < 0 || graph_id >= (int)c->graphs.size() || !c->graphs[graph_id]) return bh::fail(BH_ERR, "bad graph id");
+  BH_HIP(hipGraphLaunch(c->graphs[graph_id], c->stream));
+  return BH_OK;
+}
+
+int bh_graph_destroy(bh_ctx *c, int graph_id) {
+  BH_CHECK_CTX(c);
+  if (graph_id < 0 || graph_id >= (int)c->graphs.size() || !c->graphs[graph_id]) return bh::fail(BH_ERR, "bad graph id");
+  BH_HIP(hipStreamSynchronize(c->stream));
+  BH_HIP(hipGraphExecDestroy(c->graphs[graph_id]));
+  c->graphs[graph_id] = nullptr;
   return BH_OK;
 }
 

@@ -71,6 +71,22 @@ int bh_sync(bh_ctx *ctx);
 int bh_event_record(bh_ctx *ctx, int *event_id);
 int bh_elapsed_ms(bh_ctx *ctx, int begin_id, int end_id, float *ms);
 int bh_events_reset(bh_ctx *ctx);
+/* device timestamps, usable inside captured graphs: bh_stamp enqueues a write
+ * of the GPU's constant-rate wall clock into slot (0 <= slot < 262144);
+ * bh_stamps_read syncs and returns slots first..first+n-1 in microseconds
+ * relative to slot first. */
+int bh_stamp(bh_ctx *ctx, int slot);
+int bh_stamps_read(bh_ctx *ctx, int first, int n, double *us);
+
+/* ---- launch batching: capture everything issued on the context between
+ *      begin and end (kernels, event records) into a hipGraph and replay it
+ *      with one call, so a sweep of small ops is not bound by host launch
+ *      latency. Nothing may allocate while capturing (run one eager pass
+ *      first so split-K workspaces exist). ---------------------------------- */
+int bh_capture_begin(bh_ctx *ctx);
+int bh_capture_end(bh_ctx *ctx, int *graph_id);
+int bh_graph_launch(bh_ctx *ctx, int graph_id);
+int bh_graph_destroy(bh_ctx *ctx, int graph_id);
 
 /* ---- deterministic test data on the device: the gen_data_* kernels
  *      (test/rtc/gen-util.h:1-9, gen_data_sgemm_{a,b}.cucl,

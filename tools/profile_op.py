@@ -31,15 +31,24 @@ def main():
     if a.cfg:
         dev.tune_set(kind, boda_hip.tune_cfg_names(kind).index(a.cfg), a.splits)
     wl = runner.Workload(dev, [s])
-    ev = []
+    wl.launch(0)
+    dev.capture_begin()
+    dev.stamp(0)
     for _ in range(a.iters):
-        b = dev.event()
         wl.launch(0)
-        e = dev.event()
-        ev.append((b, e))
-    dev.sync()
-    ts = sorted(dev.elapsed_ms(b, e) for b, e in ev)
-    med = ts[len(ts) // 2]
+    dev.stamp(1)
+    g = dev.capture_end()
+    per = []
+    for _ in range(5):
+        dev.graph_launch(g)
+        t = dev.stamps_read(0, 2)
+        per.append((t[1] - t[0]) / a.iters / 1e3)
+    med = sorted(per)[2]
+    # eager event-timed single launch for comparison (the reference's convention)
+    b = dev.event()
+    wl.launch(0)
+    e = dev.event()
+    print("eager event-timed launch: %.4f ms" % dev.elapsed_ms(b, e))
     print("%s %s cfg=%s splits=%d variant=%s median %.4f ms  %.2f TFLOP/s  roofline %.1f%%" % (
         a.kind, a.dims, a.cfg or "auto", a.splits, boda_hip.variant_name(kind, d), med, s.flops() / med / 1e9,
         100 * runner.roofline_secs(s) * 1e3 / med))
