@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 import boda_hip  # noqa: E402
 from boda_hip import ops, runner  # noqa: E402
+from boda_hip.shard import Dist, lpt_partition  # noqa: E402
 
 OPS_DIR = os.path.join(ROOT, "tests", "golden", "ops")
 SETS = {
@@ -57,54 +58,6 @@ def load_sets(names):
             shapes.append(ops.shape_of(op))
             tags.append(n)
     return shapes, tags
-
-
-def lpt_partition(costs, n):
-    """Greedy longest-processing-time assignment of items to n bins; returns a list of index lists."""
-    bins = [[] for _ in range(n)]
-    load = [0.0] * n
-    for i in sorted(range(len(costs)), key=lambda i: -costs[i]):
-        j = min(range(n), key=lambda j: load[j])
-        bins[j].append(i)
-        load[j] += costs[i]
-    return [sorted(b) for b in bins]
-
-
-class Dist:
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.dist = None
-        if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            self.dist = dist
-
-    def barrier(self):
-        if self.dist:
-            self.dist.barrier()
-
-    def max(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
-
-    def close(self):
-        if self.dist:
-            self.dist.destroy_process_group()
 
 
 def cpu_baseline(budget_s):
@@ -161,7 +114,8 @@ def main():
     my_shapes = [shapes[i] for i in mine]
     my_tags = [tags[i] for i in mine]
 
-    dev = boda_hip.Device(dd.local_rank)
+    # one GPU per rank; ranks beyond the node's GPU count share (rehearsal on a 1-GPU box)
+    dev = boda_hip.Device(dd.local_rank % max(1, boda_hip.device_count()))
     wl = runner.Workload(dev, my_shapes, mode=5, tags=my_tags)
     for _ in range(args.warmup):
         wl.step()

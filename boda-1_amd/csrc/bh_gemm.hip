@@ -745,7 +745,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
   if (S > 1) {
     uint64_t nblk = (uint64_t)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
     int red = ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2);
-    s += "_splitk" + std::to_string(S) + (red == 1 ? "k" : "i");
+    s += red == 1 ? "_splitk_reduce" : "_splitk_inkernel";  // one name per kernel instantiation
   }
   return s;
 }

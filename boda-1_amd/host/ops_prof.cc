@@ -75,6 +75,40 @@ bool same_op(op_base_t const &a, op_base_t const &b) {
   return true;
 }
 
+// Greedy LPT over the op list by roofline time (same algorithm as boda_hip.shard.lpt_partition):
+// ops by descending cost (stable), each to the least-loaded shard (lowest index on ties).
+std::vector<bool> lpt_mine(std::vector<std::string> const &lines, std::string const &spec) {
+  size_t sl = spec.find('/');
+  if (sl == std::string::npos) rt_err("--shard wants k/n");
+  uint32_t k = std::stoul(spec.substr(0, sl)), n = std::stoul(spec.substr(sl + 1));
+  if (!n || k >= n) rt_err("--shard: need 0 <= k < n");
+  std::vector<std::pair<double, size_t>> cost;
+  for (size_t i = 0; i < lines.size(); ++i) {
+    op_base_t op = parse_op_line(lines[i]);
+    double c = (op.type == "Convolution" || op.type == "sgemm") ? roofline_secs(op_work(op)) : 0.0;
+    cost.emplace_back(c, i);
+  }
+  std::stable_sort(cost.begin(), cost.end(), [](auto const &x, auto const &y) { return x.first > y.first; });
+  std::vector<double> load(n, 0.0);
+  std::vector<bool> mine(lines.size(), false);
+  for (auto const &c : cost) {
+    size_t j = std::min_element(load.begin(), load.end()) - load.begin();
+    load[j] += c.first;
+    mine[c.second] = (j == k);
+  }
+  return mine;
+}
+
+std::vector<std::string> read_lines(std::string const &fn) {
+  std::ifstream f(fn);
+  if (!f) rt_err("cannot open " + fn);
+  std::vector<std::string> lines;
+  std::string l;
+  while (std::getline(f, l))
+    if (!l.empty()) lines.push_back(l);
+  return lines;
+}
+
 std::vector<std::string> arg_vars(op_base_t const &op) {
   if (op.type == "Convolution") return {"in", "filts", "biases", "out"};
   return {"a", "b", "c"};
@@ -121,10 +155,16 @@ int main(int argc, char **argv) {
       return 0;
     }
     std::string ops_fn = o.get("ops-fn");
+    if (o.kv.count("list-shard")) {  // GPU-free: the op indices shard k/n would run
+      std::vector<bool> m = lpt_mine(read_lines(ops_fn), o.get("list-shard"));
+      for (size_t i = 0; i < m.size(); ++i)
+        if (m[i]) std::printf("%zu\n", i);
+      return 0;
+    }
     if (ops_fn.empty()) {
       std::cerr << "usage: boda_hip_ops_prof --ops-fn=F [--wisdom-in-fn=F] [--wisdom-out-fn=F] [--out-fn=F]\n"
                    "  [--gen-data-mode=5] [--run-iter=1] [--mrd-toler=2e-4] [--device=0] [--write-runs=0]\n"
-                   "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F\n";
+                   "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F | --list-shard=k/n --ops-fn=F\n";
       return 2;
     }
     const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
@@ -147,39 +187,16 @@ int main(int argc, char **argv) {
     if (!o.get("wisdom-out-fn").empty()) wout.open(o.get("wisdom-out-fn"));
 
     // every line of the list (the wisdom file has one block per line, whatever the type)
-    std::vector<std::string> lines;
-    {
-      std::ifstream f(ops_fn);
-      if (!f) rt_err("cannot open " + ops_fn);
-      std::string l;
-      while (std::getline(f, l))
-        if (!l.empty()) lines.push_back(l);
-    }
+    std::vector<std::string> lines = read_lines(ops_fn);
     // optional LPT shard by roofline time
     std::vector<bool> mine(lines.size(), true);
-    std::string shard = o.get("shard");
-    if (!shard.empty()) {
-      uint32_t k = std::stoul(shard.substr(0, shard.find('/'))), n = std::stoul(shard.substr(shard.find('/') + 1));
-      std::vector<std::pair<double, size_t>> cost;
-      for (size_t i = 0; i < lines.size(); ++i) {
-        op_base_t op = parse_op_line(lines[i]);
-        double c = (op.type == "Convolution" || op.type == "sgemm") ? roofline_secs(op_work(op)) : 0.0;
-        cost.emplace_back(c, i);
-      }
-      std::stable_sort(cost.begin(), cost.end(), [](auto const &x, auto const &y) { return x.first > y.first; });
-      std::vector<double> load(n, 0.0);
-      for (auto const &c : cost) {
-        size_t j = std::min_element(load.begin(), load.end()) - load.begin();
-        load[j] += c.first;
-        mine[c.second] = (j == k);
-      }
-    }
+    if (!o.get("shard").empty()) mine = lpt_mine(lines, o.get("shard"));
 
     p_rtc_compute_t rtc = make_hip_compute(std::stoi(o.get("device", "0")));
     rtc->init();
     const std::string plat = rtc->get_plat_tag();
     const std::string tune = "(use_be=hip)";
-    uint32_t num_fail = 0, n_run = 0;
+    uint32_t num_fail = 0, n_run = 0, n_unsup = 0;
     double sum_flops = 0, sum_secs = 0, sum_roof = 0;
     for (size_t ix = 0; ix < lines.size(); ++ix) {
       op_wisdom_t wi;
@@ -222,6 +239,7 @@ int main(int argc, char **argv) {
         run.op_line = op.line;
       } catch (unsup_exception const &e) {
         err << "profile call failure: " << e.what();
+        ++n_unsup;  // recorded, not a MAD failure (src/rtc_prof.cc:287-296, :368-369)
       }
       for (auto const &vn : arg_vars(op))
         if (op.has_dims(vn)) {
@@ -265,7 +283,7 @@ int main(int argc, char **argv) {
       }
       run.err = err.str();
       if (!run.err.empty()) {
-        ++num_fail;
+        if (dstat == "FAIL") ++num_fail;
         *out << "-----\n errors for op_ix=" << ix << " op='" << lines[ix] << "'\n--  comp fail for op_tune='" << tune
              << "'\n" << run.err << "\n" << err_extra.str();
       }
@@ -283,6 +301,7 @@ int main(int argc, char **argv) {
                     plat.c_str());
       *out << buf;
     }
+    if (n_unsup) *out << "unsupported (recorded in wisdom, skipped): " << n_unsup << "\n";
     if (!num_fail) *out << "***ALL IS WELL***\n";
     else *out << "***MAD FAILS*** num_mad_fail=" << num_fail << "\n";
     return num_fail ? 1 : 0;
