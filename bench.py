@@ -14,8 +14,8 @@ device with the reference's gen_data mode 5 before the timed region).
   launch      = each timed step is a captured hipGraph (no host launch latency
                 between ops; --eager for op-by-op launches from Python)
   roofline    = the dominant kernel (most time): algorithmic flops per launch / its
-                average launch duration measured on its stream (device timestamps
-                between ops inside the replayed graph), vs fp32 peak
+                average launch duration, measured with HIP events recorded on the
+                kernel's own dispatches (hipExtLaunchKernel) on its stream, vs fp32 peak
   cpu_baseline= the oracle's fp32 OpenMP CPU implementation (kind "port") on a
                 bounded sample, rank 0 at N=1 only
 
@@ -121,19 +121,16 @@ def main():
         wl.step()
     dev.sync()
 
-    # one captured hipGraph per timed step, with a device timestamp between ops
-    # (--eager: launch op by op from Python, timed with HIP event pairs)
+    # Timed region: K steps, each a captured hipGraph of the whole op sweep, replayed
+    # back to back (--eager: launched op by op from Python instead).
     nop = len(my_shapes)
-    graphs, events = [], []
-    if not args.eager:
-        for k in range(args.steps):
-            graphs.append(wl.capture_step(stamp_base=k * (nop + 1)))
+    graphs = [] if args.eager else [wl.capture_step() for _ in range(args.steps)]
     dd.barrier()
     dev.sync()
     t0 = time.perf_counter()
     if args.eager:
         for _ in range(args.steps):
-            wl.step(events)
+            wl.step()
     else:
         for g in graphs:
             dev.graph_launch(g)
@@ -142,17 +139,16 @@ def main():
     dd.barrier()
     elapsed = dd.max(t1 - t0)
 
-    # per-op kernel times on the context's stream, mean over the timed steps
+    # Per-op GPU time (the reference's per-op convention, src/rtc_prof.cc:104-124): K more
+    # steps, each op timed by HIP events recorded on its own first/last kernel dispatch.
+    events = []
+    for _ in range(args.steps):
+        wl.step_kernel_timed(events)
+    dev.sync()
     ktime = [0.0] * nop
-    if args.eager:
-        for i, b, e in events:
-            ktime[i] += dev.elapsed_ms(b, e) / 1e3
-        dev.events_reset()
-    else:
-        ts = dev.stamps_read(0, args.steps * (nop + 1))
-        for k in range(args.steps):
-            for i in range(nop):
-                ktime[i] += (ts[k * (nop + 1) + i + 1] - ts[k * (nop + 1) + i]) / 1e6
+    for i, b, e in events:
+        ktime[i] += dev.elapsed_ms(b, e) / 1e3
+    dev.events_reset()
     ktime = [t / args.steps for t in ktime]
 
     my_flops = sum(s.flops() for s in my_shapes)
@@ -220,8 +216,8 @@ def main():
             "dtype": "f32", "data": "synthetic (reference gen_data mode 5, generated on device)",
             "config": {"workload": " + ".join(SETS[n] for n in set_names) + " (one main-kernel launch per op per step)",
                        "launch": "eager" if args.eager else "hipGraph replay of each step",
-                       "op_timing": "HIP event pair per op" if args.eager else
-                       "device wall-clock stamp between ops inside the graph (op + one stamp + seams)",
+                       "op_timing": "HIP events on each op's first/last kernel dispatch (hipExtLaunchKernel), "
+                                    "K extra eager steps after the timed region",
                        "ops_per_gpu": len(my_shapes), "gflop_per_step_per_gpu": round(my_flops / 1e9, 3),
                        "parallelism": ("op-shard" if args.strong else "op-replica") + "%d" % dd.world,
                        "plat": dev.plat_tag()},

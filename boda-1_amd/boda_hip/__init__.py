@@ -24,7 +24,7 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
            "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
-           "bh_stamp", "bh_stamps_read"]
+           "bh_stamp", "bh_stamps_read", "bh_time_next_call"]
 
 
 class BodaHipError(RuntimeError):
@@ -70,6 +70,7 @@ def lib():
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
         L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
+        L.bh_time_next_call.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.bh_stamps_read.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.bh_capture_begin.argtypes = [c_vp]
         L.bh_capture_end.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int)]
@@ -198,6 +199,12 @@ class Device:
         d = list(dims) + [1] * (4 - len(dims))
         arr = (c_u32 * 4)(*d)
         _check(lib().bh_gen_data(self.ctx, kind, buf.ptr, arr, mode, vi))
+
+    def time_next_call(self):
+        """Arm kernel-dispatch events for the next call; returns (begin id, end id)."""
+        b, e = ctypes.c_int(-1), ctypes.c_int(-1)
+        _check(lib().bh_time_next_call(self.ctx, ctypes.byref(b), ctypes.byref(e)))
+        return b.value, e.value
 
     def stamp(self, slot):
         _check(lib().bh_stamp(self.ctx, slot))

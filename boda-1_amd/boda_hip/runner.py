@@ -92,6 +92,14 @@ class Workload:
         if stamp_base is not None:
             self.dev.stamp(stamp_base + len(self.ops))
 
+    def step_kernel_timed(self, out):
+        """One eager pass; each op's GPU time is recorded on its own first/last kernel
+        dispatch (bh_time_next_call). Appends (op index, begin event, end event) to out."""
+        for i in range(len(self.ops)):
+            b, e = self.dev.time_next_call()
+            self.launch(i)
+            out.append((i, b, e))
+
     def capture_step(self, stamp_base=None):
         """Capture one step into a hipGraph (HIP events cannot be timed inside graphs,
         so per-op times come from device stamps, see step()). Returns the graph id."""

@@ -1,6 +1,7 @@
 // bh_common.h -- internal declarations shared by the libboda_hip.so sources.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <algorithm>
 #include <dlfcn.h>
@@ -23,6 +24,8 @@ struct bh_ctx {
   int ovr_red[2] = {0, 0};
   std::vector<hipGraphExec_t> graphs;  // captured launch sequences
   void *stamps = nullptr;              // device timestamp slots (bh_stamp)
+  hipEvent_t t_start = nullptr;        // bh_time_next_call: events for the next call's
+  hipEvent_t t_stop = nullptr;         //   first / last kernel dispatch
   double stamp_hz = 100e6;
   void *cnt = nullptr;  // split-K arrival tickets
   uint64_t cnt_n = 0;
@@ -35,6 +38,12 @@ int ok();                                    // clears nothing, returns BH_OK
 
 // Kernel launch checks (hipGetLastError after each launch).
 int check_launch(const char *what);
+
+// Launch on the context's stream; when bh_time_next_call armed an event pair, the
+// first dispatch of the call records the start event and the last one the stop
+// event on the kernel's own dispatch (hipExtLaunchKernel).
+int launch(bh_ctx *ctx, const void *kernel, dim3 grid, dim3 block, void **args, bool first, bool last,
+           const char *what);
 
 // Magic-number unsigned division for 0 <= n < 2^31, 1 <= d < 2^31:
 // q = (umulhi(n, m) + n) >> s.

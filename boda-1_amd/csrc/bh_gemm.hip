@@ -110,19 +110,39 @@ __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
 // order s = 0..S-1 (bitwise reproducible whoever combines), add bias, ReLU, store
 // to the dense C or scatter to NCHW. Used by the reduce kernel and by the last-
 // arriving block of a tile. chunk c covers tile elements 4c..4c+3 (row-major BM x BN).
-template <int IMODE>
+constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
+
+// SC1: the slabs were handed off inside this launch (in-kernel combine): every load of
+// them is an sc1 buffer load (the producers stored them sc1 and drained before their
+// ticket), per the split-K recipe of cdna_hip_programming.md §5. Otherwise (reduce
+// kernel after a kernel boundary) plain loads.
+template <int IMODE, bool SC1>
 __device__ __forceinline__ void combine_store(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
                                               uint32_t c, uint32_t S, const float *bias_lds) {
   const size_t tsz = (size_t)p.tbm * p.tbn, slab = tsz * p.tiles_m * p.tiles_n;
-  const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
   f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t q = 0;
-  for (; q + 4 <= S; q += 4) {  // four slabs in flight
-    f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
-    f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
-    sum += a0; sum += a1; sum += a2; sum += a3;
+  if constexpr (SC1) {
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws, 0x7fffff00u);
+    const uint32_t base = (uint32_t)(((size_t)tile * tsz + 4 * c) * 4), sstep = (uint32_t)(slab * 4);
+    for (; q + 4 <= S; q += 4) {  // four slabs in flight
+      f32x4v a0 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 0) * sstep, 0, AUX_SC1));
+      f32x4v a1 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 1) * sstep, 0, AUX_SC1));
+      f32x4v a2 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 2) * sstep, 0, AUX_SC1));
+      f32x4v a3 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 3) * sstep, 0, AUX_SC1));
+      sum += a0; sum += a1; sum += a2; sum += a3;
+    }
+    for (; q < S; ++q)
+      sum += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + q * sstep, 0, AUX_SC1));
+  } else {
+    const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
+    for (; q + 4 <= S; q += 4) {  // four slabs in flight
+      f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
+      f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
+      sum += a0; sum += a1; sum += a2; sum += a3;
+    }
+    for (; q < S; ++q) sum += src[q * slab / 4];
   }
-  for (; q < S; ++q) sum += src[q * slab / 4];
   const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
   const uint32_t m = tile_m * p.tbm + row;
   if (m >= p.M) return;
@@ -373,42 +393,51 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   if constexpr (SPLIT) {
     // raw partial sums -> this split's slab of this tile (tile-major, row-major BM x BN)
     const uint32_t tile = tile_m * p.tiles_n + tile_n;
-    float *const wz = p.ws + ((size_t)split * p.tiles_m * p.tiles_n + tile) * (BM * BN);
+    const size_t slab_off = ((size_t)split * p.tiles_m * p.tiles_n + tile) * (BM * BN);
+    float *const wz = p.ws + slab_off;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(wz, BM * BN * 4);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm * WM + TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+        const uint32_t off = row * BN + wn * WN + TN * li;
         typename fvec<TN>::t w;
         if constexpr (TN == 1) w = acc[i][0][r]; else {
 #pragma unroll
           for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
         }
-        *(typename fvec<TN>::t *)&wz[row * BN + wn * WN + TN * li] = w;
+        if constexpr (SPL == 1) {
+          *(typename fvec<TN>::t *)&wz[off] = w;
+        } else if constexpr (TN == 1) {  // write-through (sc1): handed off inside this launch
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, w), rw, off * 4, 0, AUX_SC1);
+        } else if constexpr (TN == 2) {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) uint32_t, w),
+                                                rw, off * 4, 0, AUX_SC1);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, w),
+                                                 rw, off * 4, 0, AUX_SC1);
+        }
       }
     if constexpr (SPL == 1) return;  // bias / ReLU / NCHW scatter happen in splitk_reduce_kernel
-    // Publish the slab and count arrivals (cdna_hip_programming.md split-K recipe):
-    // every storing wave drains, barrier, one agent-scope release, then the ticket.
-    // The block drawing S-1 acquires and combines all S slabs of the tile.
+    // Publish the slab and count arrivals (cdna_hip_programming.md §5 split-K recipe, the
+    // write-through form): sc1 slab stores, every storing wave drains them, barrier, one
+    // lane takes a relaxed agent-scope ticket. The block drawing S-1 combines all S slabs
+    // reading every one of them with sc1 loads -- no release / acquire fences needed.
     uint32_t *const flag = (uint32_t *)smem;  // the A/B tiles are dead after the loop's last barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
-      if (last) {
-        __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
       *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
     for (uint32_t c = tid; c < BM * BN / 4; c += NT)
-      combine_store<IM ? 1 : 0>(p, tile, tile_m, tile_n, c, gridDim.y, IM ? Lbias : nullptr);
+      combine_store<IM ? 1 : 0, true>(p, tile, tile_m, tile_n, c, gridDim.y, IM ? Lbias : nullptr);
     return;
   }
   int cofs[TN];
@@ -467,7 +496,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p, uint32_t
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t tile = (uint32_t)(e / per_tile), c = (uint32_t)(e - (uint64_t)tile * per_tile);
     const uint32_t tile_m = tile / p.tiles_n, tile_n = tile - tile_m * p.tiles_n;
-    combine_store<IMODE>(p, tile, tile_m, tile_n, c, S, nullptr);
+    combine_store<IMODE, false>(p, tile, tile_m, tile_n, c, S, nullptr);
   }
 }
 
@@ -691,7 +720,8 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   p.ks = ((nkt + S - 1) / S) * c.BK;
   // in-kernel combine unless asked otherwise or the tile grid is large (then a separate,
   // fully parallel reduce pass is cheaper than serial combining by last arrivers)
-  const int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2));
+  int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2));
+  if (red == 2 && (uint64_t)S * nblk * c.BM * c.BN * 4 >= 0x7fffff00ull) red = 1;  // sc1 offsets are 32-bit
   kern_t k = c.k[ald][bld][red];
   if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
   void *args[] = {&p};
@@ -705,20 +735,19 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
       rc = ensure_cnt(ctx, nblk);
       if (rc != BH_OK) return rc;
       p.cnt = (uint32_t *)ctx->cnt;
-      BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, 0, ctx->stream));
-      return bh::check_launch(what);
+      return bh::launch(ctx, (const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, true, true, what);
     }
-    BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, 0, ctx->stream));
+    rc = bh::launch(ctx, (const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, true, false, what);
+    if (rc != BH_OK) return rc;
     const uint64_t total = nblk * c.BM * c.BN / 4;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
-    if (bld == B_IM2COL || bld == B_IM1X1)
-      hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3(grid), dim3(256), 0, ctx->stream, p, S);
-    else
-      hipLaunchKernelGGL(splitk_reduce_kernel<0>, dim3(grid), dim3(256), 0, ctx->stream, p, S);
-    return bh::check_launch("splitk_reduce");
+    const void *rk = (bld == B_IM2COL || bld == B_IM1X1) ? (const void *)splitk_reduce_kernel<1>
+                                                          : (const void *)splitk_reduce_kernel<0>;
+    uint32_t Sv = S;
+    void *rargs[] = {&p, &Sv};
+    return bh::launch(ctx, rk, dim3(grid), dim3(256), rargs, false, true, "splitk_reduce");
   }
-  BH_HIP(hipLaunchKernel((const void *)k, dim3((uint32_t)nblk, 1, 1), dim3(c.NT), args, 0, ctx->stream));
-  return bh::check_launch(what);
+  return bh::launch(ctx, (const void *)k, dim3((uint32_t)nblk, 1, 1), dim3(c.NT), args, true, true, what);
 }
 
 void conv_dims(const uint32_t *d, uint32_t &M, uint32_t &N, uint32_t &K) {
@@ -745,6 +774,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
   if (S > 1) {
     uint64_t nblk = (uint64_t)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
     int red = ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2);
+    if (red == 2 && (uint64_t)S * nblk * c.BM * c.BN * 4 >= 0x7fffff00ull) red = 1;
     s += red == 1 ? "_splitk_reduce" : "_splitk_inkernel";  // one name per kernel instantiation
   }
   return s;

@@ -122,7 +122,7 @@ int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], u
   if (!g.n) return BH_OK;
   uint64_t want = (g.n / 4 + 255) / 256;
   uint32_t grid = (uint32_t)(want < 2048 ? (want ? want : 1) : 2048);
-  hipLaunchKernelGGL(gen_data_kernel, dim3(grid), dim3(256), 0, ctx->stream, g);
-  return check_launch("gen_data");
+  void *args[] = {&g};
+  return launch(ctx, (const void *)gen_data_kernel, dim3(grid), dim3(256), args, true, true, "gen_data");
 }
 }  // namespace bh

@@ -33,6 +33,17 @@ int check_launch(const char *what) {
   if (e != hipSuccess) return fail(BH_ERR, std::string("launch of ") + what + " failed: " + hipGetErrorString(e));
   return BH_OK;
 }
+
+int launch(bh_ctx *ctx, const void *kernel, dim3 grid, dim3 block, void **args, bool first, bool last,
+           const char *what) {
+  hipEvent_t b = first ? ctx->t_start : nullptr, e = last ? ctx->t_stop : nullptr;
+  hipError_t r = (b || e) ? hipExtLaunchKernel(kernel, grid, block, args, 0, ctx->stream, b, e, 0)
+                          : hipLaunchKernel(kernel, grid, block, args, 0, ctx->stream);
+  if (first) ctx->t_start = nullptr;
+  if (last) ctx->t_stop = nullptr;
+  if (r != hipSuccess) return fail(BH_ERR, std::string("launch of ") + what + " failed: " + hipGetErrorString(r));
+  return check_launch(what);
+}
 }  // namespace bh
 
 extern "C" {
@@ -175,6 +186,22 @@ int bh_event_record(bh_ctx *c, int *id) {
   return BH_OK;
 }
 
+int bh_time_next_call(bh_ctx *c, int *begin_id, int *end_id) {
+  BH_CHECK_CTX(c);
+  if (!begin_id || !end_id) return bh::fail(BH_ERR, "null out");
+  for (int k = 0; k < 2; ++k)
+    if (c->events_used + k >= (int)c->events.size()) {
+      hipEvent_t ev;
+      BH_HIP(hipEventCreate(&ev));
+      c->events.push_back(ev);
+    }
+  *begin_id = c->events_used++;
+  *end_id = c->events_used++;
+  c->t_start = c->events[*begin_id];
+  c->t_stop = c->events[*end_id];
+  return BH_OK;
+}
+
 int bh_elapsed_ms(bh_ctx *c, int b, int e, float *ms) {
   BH_CHECK_CTX(c);
   if (!ms) return bh::fail(BH_ERR, "null out");
@@ -227,7 +254,9 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
 int bh_stamp(bh_ctx *c, int slot) {
   BH_CHECK_CTX(c);
   if (slot < 0 || slot >= STAMP_SLOTS) return bh::fail(BH_ERR, "stamp slot out of range");
-  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, c->stream, (unsigned long long *)c->stamps, slot);
+  unsigned long long *t = (unsigned long long *)c->stamps;
+  void *args[] = {&t, &slot};
+  BH_HIP(hipLaunchKernel((const void *)stamp_kernel, dim3(1), dim3(64), args, 0, c->stream));
   return bh::check_launch("stamp");
 }
 

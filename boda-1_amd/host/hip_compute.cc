@@ -4,8 +4,10 @@
 // Contract followed (nvrtc_compute_t, src/nvrtc_util.cc:174-395):
 //   * vars are device buffers keyed by name, zero-filled at creation (:80-84);
 //     reshaped views share the buffer (src/rtc_compute.cc:29-41);
-//   * run() brackets each call with a begin/end event pair and returns a call id;
-//     get_dur(b,e) is begin(b) -> end(e) in milliseconds (:289-298, :367-381);
+//   * run() attaches a begin/end event pair to each call and returns a call id;
+//     get_dur(b,e) is begin(b) -> end(e) in milliseconds (:289-298, :367-381). The
+//     events are recorded on the call's own first/last kernel dispatch
+//     (bh_time_next_call), so host launch latency is not part of the duration;
 //   * the hot ops are hand-written kernels reached by function name, the way
 //     the reference reaches cuBLAS/cuDNN through its culibs intercept
 //     (src/nvrtc_util.cc:369-372): hip_sgemm, hip_conv, and the gen_data_*
@@ -133,7 +135,8 @@ struct hip_compute_t : public rtc_compute_t {
     if (fit == funcs.end()) rt_err("hip_compute: function '" + rfc.rtc_func_name + "' not compiled");
     rtc_func_info_t const &fi = fit->second;
     call_ev_t ev{};
-    bh_check(bh_event_record(ctx, &ev.b), "bh_event_record");
+    // events on the call's own first/last kernel dispatch (no host launch latency)
+    bh_check(bh_time_next_call(ctx, &ev.b, &ev.e), "bh_time_next_call");
     std::string const &fn = fi.func_name;
     if (fn == "hip_sgemm") {
       dims_t const &a = arg_dims(rfc, "a"), &b = arg_dims(rfc, "b");
@@ -165,7 +168,6 @@ struct hip_compute_t : public rtc_compute_t {
       for (size_t i = 0; i < d.d.size(); ++i) dd[i] = d.d[i].sz;
       bh_check(bh_gen_data(ctx, kind, arg_ptr(rfc, an), dd, mode, vi), fn);
     }
-    bh_check(bh_event_record(ctx, &ev.e), "bh_event_record");
     calls.push_back(ev);
     return (uint32_t)(calls.size() - 1);
   }

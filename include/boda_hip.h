@@ -71,6 +71,11 @@ int bh_sync(bh_ctx *ctx);
 int bh_event_record(bh_ctx *ctx, int *event_id);
 int bh_elapsed_ms(bh_ctx *ctx, int begin_id, int end_id, float *ms);
 int bh_events_reset(bh_ctx *ctx);
+/* arm an event pair for the NEXT hot-path / gen_data call on this context: its
+ * first kernel dispatch records begin_id, its last records end_id, on the
+ * dispatches themselves (hipExtLaunchKernel), so bh_elapsed_ms(begin, end) is the
+ * call's GPU time (split-K reduce pass included) without host launch latency. */
+int bh_time_next_call(bh_ctx *ctx, int *begin_id, int *end_id);
 /* device timestamps, usable inside captured graphs: bh_stamp enqueues a write
  * of the GPU's constant-rate wall clock into slot (0 <= slot < 262144);
  * bh_stamps_read syncs and returns slots first..first+n-1 in microseconds

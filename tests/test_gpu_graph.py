@@ -34,3 +34,30 @@ def test_graph_replay_matches_eager(dev):
     assert all(b > a for a, b in zip(ts, ts[1:]))  # stamps advance between ops
     dev.graph_destroy(g)
     wl.free()
+
+
+def test_time_next_call_covers_split_k_reduce(dev):
+    """bh_time_next_call's events sit on the call's own first and last dispatch: positive,
+    and not longer than a host-side event pair around the same call."""
+    s = ops.ConvShape(1, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)
+    wl = runner.Workload(dev, [s])
+    dev.tune_set(1, 0, -8)  # 8 splits combined by the separate reduce kernel: two dispatches
+    try:
+        wl.launch(0)
+        t_kernel, t_pair = [], []
+        for _ in range(5):
+            b, e = dev.time_next_call()
+            wl.launch(0)
+            dev.sync()
+            t_kernel.append(dev.elapsed_ms(b, e))
+            b2 = dev.event()
+            wl.launch(0)
+            e2 = dev.event()
+            dev.sync()
+            t_pair.append(dev.elapsed_ms(b2, e2))
+        dev.events_reset()
+        assert min(t_kernel) > 0
+        assert sorted(t_kernel)[2] <= sorted(t_pair)[2] * 1.05
+    finally:
+        dev.tune_set(1, -1, 0)
+        wl.free()

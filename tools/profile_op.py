@@ -44,11 +44,14 @@ def main():
         t = dev.stamps_read(0, 2)
         per.append((t[1] - t[0]) / a.iters / 1e3)
     med = sorted(per)[2]
-    # eager event-timed single launch for comparison (the reference's convention)
-    b = dev.event()
-    wl.launch(0)
-    e = dev.event()
-    print("eager event-timed launch: %.4f ms" % dev.elapsed_ms(b, e))
+    # eager launches timed on their own kernel dispatches
+    ev = []
+    for _ in range(5):
+        ev.append(dev.time_next_call())
+        wl.launch(0)
+    dev.sync()
+    kt = sorted(dev.elapsed_ms(b, e) for b, e in ev)
+    print("kernel-dispatch timed call (median of 5): %.4f ms; back-to-back in a graph (below): per launch" % kt[2])
     print("%s %s cfg=%s splits=%d variant=%s median %.4f ms  %.2f TFLOP/s  roofline %.1f%%" % (
         a.kind, a.dims, a.cfg or "auto", a.splits, boda_hip.variant_name(kind, d), med, s.flops() / med / 1e9,
         100 * runner.roofline_secs(s) * 1e3 / med))

@@ -4,8 +4,8 @@
 The backend's counterpart of Boda's op_tune sweeps + wisdom (src/rtc_prof.cc
 ops-prof over several --op-tunes; src/op-tuner.cc): for every op of the given
 op lists, time each instantiated tile configuration with each split count
-(median over --reps launches in a captured graph, each between device stamps
-after a cache flush), keep the fastest and
+(median over --reps calls, each after a cache flush, timed by events on the
+call's own kernel dispatches), keep the fastest and
 write boda-1_amd/tuning/gfx950.tune lines "<op> <dims> cfg=<name> splits=<n>".
 Results of every candidate go to --json for analysis.
 
@@ -41,26 +41,26 @@ FLUSH = None
 
 
 def time_op(dev, wl, i, reps):
-    """Median time of one launch (ms) as the bench sees it: a captured graph of `reps`
-    launches, each between two device stamps and preceded by a 512 MiB memset that
-    evicts L2 and the Infinity Cache (in the bench every op runs after 220 others)."""
+    """Median GPU time of one call (ms) as the bench sees it: each launch preceded by a
+    512 MiB memset that evicts L2 and the Infinity Cache (in the bench every op runs after
+    220 others), timed by events on the call's own kernel dispatches."""
     global FLUSH
     if FLUSH is None:
         FLUSH = dev.alloc(512 << 20)
-    wl.launch(i)  # eager warm-up (grows the split-K workspace before capture)
-    dev.capture_begin()
-    try:
-        for r in range(reps):
-            FLUSH.zero()
-            dev.stamp(2 * r)
-            wl.launch(i)
-            dev.stamp(2 * r + 1)
-    finally:
-        g = dev.capture_end()
-    dev.graph_launch(g)
-    t = dev.stamps_read(0, 2 * reps)
-    dev.graph_destroy(g)
-    return statistics.median((t[2 * r + 1] - t[2 * r]) / 1e3 for r in range(reps))
+    wl.launch(i)  # warm-up (grows the split-K workspace)
+    ev = []
+    for _ in range(reps):
+        FLUSH.zero()
+        b, e = dev.time_next_call()
+        wl.launch(i)
+        ev.append((b, e))
+    dev.sync()
+    out = [dev.elapsed_ms(b, e) for b, e in ev]
+    dev.events_reset()
+    return statistics.median(out)
+
+
+FLUSH = None
 
 
 def main():
