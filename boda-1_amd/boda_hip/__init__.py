@@ -13,7 +13,8 @@ from . import ops  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libboda_hip.so")
+# BH_LIB_NAME selects an alternative in-tree build (e.g. libboda_hip_ktrace.so, tools/ktrace.py)
+LIB_PATH = os.path.join(PKG, "lib", os.environ.get("BH_LIB_NAME", "libboda_hip.so"))
 
 BH_OK, BH_ERR, BH_UNSUP = 0, 1, 2
 GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5)
@@ -24,7 +25,7 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
            "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
-           "bh_stamp", "bh_stamps_read", "bh_time_next_call"]
+           "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin"]
 
 
 class BodaHipError(RuntimeError):
@@ -70,6 +71,7 @@ def lib():
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
         L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
+        L.bh_spin.argtypes = [c_vp, ctypes.c_int]
         L.bh_time_next_call.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.bh_stamps_read.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.bh_capture_begin.argtypes = [c_vp]
@@ -208,6 +210,10 @@ class Device:
 
     def stamp(self, slot):
         _check(lib().bh_stamp(self.ctx, slot))
+
+    def spin(self, us):
+        """Enqueue a bounded GPU busy-wait (queue pre-fill before timed batches)."""
+        _check(lib().bh_spin(self.ctx, int(us)))
 
     def stamps_read(self, first, n):
         """Slots first..first+n-1 in microseconds relative to slot first (syncs)."""

@@ -100,6 +100,29 @@ class Workload:
             self.launch(i)
             out.append((i, b, e))
 
+    def op_graph_time(self, i, reps, spin_us=100):
+        """Amortized GPU seconds per call of op i: `reps` back-to-back calls captured in
+        one hipGraph and replayed behind a short spin kernel (so the whole batch is queued
+        before the GPU reaches it), timed by HIP events recorded around the replay on the
+        context's stream. This is the op's cost in a dense sweep (dispatch + run + drain),
+        free of the ~2.5 us that events bound to each dispatch add to a lone call."""
+        self.dev.capture_begin()
+        try:
+            for _ in range(reps):
+                self.launch(i)
+        finally:
+            g = self.dev.capture_end()
+        try:
+            self.dev.graph_launch(g)  # warm: graph upload, caches, split-K workspaces
+            self.dev.spin(spin_us)
+            b = self.dev.event()
+            self.dev.graph_launch(g)
+            e = self.dev.event()
+            self.dev.sync()
+            return self.dev.elapsed_ms(b, e) / 1e3 / reps
+        finally:
+            self.dev.graph_destroy(g)
+
     def capture_step(self, stamp_base=None):
         """Capture one step into a hipGraph (HIP events cannot be timed inside graphs,
         so per-op times come from device stamps, see step()). Returns the graph id."""

@@ -38,7 +38,10 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
-enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3 };
+enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4 };
+// B_IM1X1V: 1x1 conv whose OH*OW % 4 == 0 with a 16-B aligned input: four adjacent output
+// columns are four adjacent input pixels of one image (latency kernel only; the tile
+// kernel treats it as B_IM1X1)
 
 constexpr uint32_t OOB = 0x80000000u;  // buffer offset that always misses (extents < 2^31)
 constexpr int APAD = 4;                // m-major A tile row padding (floats)
@@ -60,7 +63,22 @@ struct GemmArgs {
   // implicit im2col (B_IM2COL / B_IM1X1); N = B*OH*OW, K = IC*KY*KX
   uint32_t H, W, KX, KYX, sy, sx, py, px, OW, OHW, HW, ICHW, OCOHW;
   uint32_t kyx_m, kyx_s, kx_m, kx_s, ohw_m, ohw_s, ow_m, ow_s;  // fastdiv constants
+#ifdef BH_KTRACE
+  unsigned long long *trace;  // per-block device-clock marks (tools/ktrace.py)
+#endif
 };
+
+#ifdef BH_KTRACE
+#define KT(k)                                                                                     \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      p.trace[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = wall_clock64();          \
+  } while (0)
+#else
+#define KT(k) \
+  do {        \
+  } while (0)
+#endif
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) {
   return (__umulhi(n, m) + n) >> s;
@@ -69,6 +87,10 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
 }
+// Offset, or the always-missing OOB offset when !ok. Callers combine conditions with
+// bitwise & (no short-circuit): a && chain lets hipcc turn the select into a branch
+// around each load, which also breaks its vmcnt bookkeeping for the ring.
+__device__ __forceinline__ uint32_t oob_unless(bool ok, uint32_t off) { return ok ? off : OOB; }
 __device__ __forceinline__ f32x4v ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
@@ -106,59 +128,111 @@ __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
   else return v[i];
 }
 
-// Split-K combine of one float4 chunk of one tile: sum the S partial slabs in fixed
-// order s = 0..S-1 (bitwise reproducible whoever combines), add bias, ReLU, store
-// to the dense C or scatter to NCHW. Used by the reduce kernel and by the last-
-// arriving block of a tile. chunk c covers tile elements 4c..4c+3 (row-major BM x BN).
+// Split-K slabs are summed in fixed order s = 0..S-1 (bitwise reproducible whoever
+// combines: the reduce kernel or a tile's last-arriving block).
+// Bias, ReLU and store of one float4 chunk c (tile elements 4c..4c+3, row-major BM x BN)
+// of tile (tile_m, tile_n): dense C rows, or NCHW scatter for conv (IMODE). p.cvec: rows
+// take aligned float4 stores (dense: ldc % 4 == 0; conv: OH*OW % 4 == 0).
+template <int IMODE>
+__device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
+                                             f32x4v sum, const float *bias_lds) {
+  const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
+  const uint32_t m = tile_m * p.tbm + row;
+  if (m >= p.M) return;
+  const float b = bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f);
+  const uint32_t n0 = tile_n * p.tbn + col0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float x = sum[t] + b;
+    sum[t] = (p.relu && x < 0.0f) ? 0.0f : x;
+  }
+  if (p.cvec && n0 + 4 <= p.N) {
+    size_t o;
+    if constexpr (IMODE) {
+      const uint32_t img = fdiv(n0, p.ohw_m, p.ohw_s);
+      o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n0 - img * p.OHW);
+    } else {
+      o = (size_t)m * p.ldc + n0;
+    }
+    *(f32x4v *)&p.c[o] = sum;
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t n = n0 + t;
+    if (n >= p.N) break;
+    if constexpr (IMODE) {
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW)] = sum[t];
+    } else {
+      p.c[(size_t)m * p.ldc + n] = sum[t];
+    }
+  }
+}
+
 constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
 
-// SC1: the slabs were handed off inside this launch (in-kernel combine): every load of
-// them is an sc1 buffer load (the producers stored them sc1 and drained before their
-// ticket), per the split-K recipe of cdna_hip_programming.md §5. Otherwise (reduce
-// kernel after a kernel boundary) plain loads.
-template <int IMODE, bool SC1>
+// Split-K combine of one float4 chunk c for the reduce kernel (after a kernel boundary,
+// so plain loads): the S slabs summed in fixed order, four in flight.
+template <int IMODE>
 __device__ __forceinline__ void combine_store(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
                                               uint32_t c, uint32_t S, const float *bias_lds) {
   const size_t tsz = (size_t)p.tbm * p.tbn, slab = tsz * p.tiles_m * p.tiles_n;
   f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t q = 0;
-  if constexpr (SC1) {
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws, 0x7fffff00u);
-    const uint32_t base = (uint32_t)(((size_t)tile * tsz + 4 * c) * 4), sstep = (uint32_t)(slab * 4);
-    for (; q + 4 <= S; q += 4) {  // four slabs in flight
-      f32x4v a0 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 0) * sstep, 0, AUX_SC1));
-      f32x4v a1 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 1) * sstep, 0, AUX_SC1));
-      f32x4v a2 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 2) * sstep, 0, AUX_SC1));
-      f32x4v a3 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + (q + 3) * sstep, 0, AUX_SC1));
-      sum += a0; sum += a1; sum += a2; sum += a3;
-    }
-    for (; q < S; ++q)
-      sum += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, base + q * sstep, 0, AUX_SC1));
-  } else {
-    const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
-    for (; q + 4 <= S; q += 4) {  // four slabs in flight
-      f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
-      f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
-      sum += a0; sum += a1; sum += a2; sum += a3;
-    }
-    for (; q < S; ++q) sum += src[q * slab / 4];
+  const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
+  for (; q + 4 <= S; q += 4) {
+    f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
+    f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
+    sum += a0; sum += a1; sum += a2; sum += a3;
   }
-  const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
-  const uint32_t m = tile_m * p.tbm + row;
-  if (m >= p.M) return;
-  const float b = bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f);
+  for (; q < S; ++q) sum += src[q * slab / 4];
+  finish_store<IMODE>(p, tile_m, tile_n, c, sum, bias_lds);
+}
+
+// In-kernel split-K combine of a whole tile by one block (the last arriver): each
+// thread owns CH float4 chunks (c = tid + j*NT), processed G at a time with all of
+// a group's loads for two slabs issued before any is consumed, so the slab reads
+// overlap instead of costing one L2 round trip per chunk. Same fixed slab order as
+// combine_store (bitwise identical results).
+template <int IMODE, int NT, int CH, int G, int NCH = CH * NT>
+__device__ __forceinline__ void combine_tile(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
+                                             uint32_t S, const float *bias_lds, int tid) {
+  static_assert(CH % G == 0, "chunk grouping");
+  if (NCH % NT != 0 && tid >= NCH) return;  // fewer chunks than threads (CH == 1)
+  const uint32_t tsz = p.tbm * p.tbn, sstep = tsz * p.tiles_m * p.tiles_n * 4;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws, 0x7fffff00u);
+#pragma unroll 1
+  for (int g = 0; g < CH; g += G) {
+    uint32_t off[G];
+    f32x4v sum[G];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const uint32_t n = tile_n * p.tbn + col0 + t;
-    if (n >= p.N) break;
-    float x = sum[t] + b;
-    if (p.relu && x < 0.0f) x = 0.0f;
-    if constexpr (IMODE) {
-      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
-      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW)] = x;
-    } else {
-      p.c[(size_t)m * p.ldc + n] = x;
+    for (int j = 0; j < G; ++j) {
+      off[j] = (tile * tsz + 4 * (uint32_t)(tid + (g + j) * NT)) * 4;
+      sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
     }
+    uint32_t q = 0;
+    for (; q + 2 <= S; q += 2) {
+      f32x4v x0[G], x1[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        x0[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
+        x1[j] = __builtin_bit_cast(f32x4v,
+                                   __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + (q + 1) * sstep, 0, AUX_SC1));
+      }
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        sum[j] += x0[j];
+        sum[j] += x1[j];
+      }
+    }
+    if (q < S) {
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        sum[j] += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) finish_store<IMODE>(p, tile_m, tile_n, (uint32_t)(tid + (g + j) * NT), sum[j], bias_lds);
   }
 }
 
@@ -186,6 +260,7 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  KT(0);
 
   uint32_t tile_m, tile_n;
   map_tile(blockIdx.x, p.tiles_m, p.tiles_n, tile_m, tile_n);
@@ -200,10 +275,10 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
 
   // ---- per-thread constants of the im2col gather (column fixed over the K loop)
   int col_base = 0, iy0 = 0, ix0 = 0;
-  bool col_ok = false;
+  uint32_t col_oob = 0;  // OOB for a column past N: or-ed into every offset (no per-load branch)
   if constexpr (IM) {
     const uint32_t col = bn0 + (uint32_t)(tid % BN);
-    col_ok = col < p.N;
+    col_oob = col < p.N ? 0u : OOB;
     const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
     const uint32_t pix = col - img * p.OHW;
     if constexpr (BLD == B_IM1X1) {
@@ -237,19 +312,19 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
         if constexpr (ALD == A_KVEC) {
           const int kr = idx / (BM / 4), mc = idx % (BM / 4);
           const uint32_t m = bm0 + 4 * mc, k = k0 + kr;
-          sa4[j] = ld4(rsa, (m < p.M && k < p.K) ? (k * p.lda + m) * 4u : OOB);
+          sa4[j] = ld4(rsa, oob_unless((m < p.M) & (k < p.K), (k * p.lda + m) * 4u));
         } else if constexpr (ALD == A_KSCALAR) {
           const int kr = idx / BM, mc = idx % BM;
           const uint32_t m = bm0 + mc, k = k0 + kr;
-          sa1[j] = ld1(rsa, (m < p.M && k < p.K) ? (k * p.lda + m) * 4u : OOB);
+          sa1[j] = ld1(rsa, oob_unless((m < p.M) & (k < p.K), (k * p.lda + m) * 4u));
         } else if constexpr (ALD == A_MVEC) {
           const int kc = idx % (BK / 4), mr = idx / (BK / 4);
           const uint32_t m = bm0 + mr, k = k0 + 4 * kc;
-          sa4[j] = ld4(rsa, (m < p.M && k < p.K) ? (m * p.lda + k) * 4u : OOB);
+          sa4[j] = ld4(rsa, oob_unless((m < p.M) & (k < p.K), (m * p.lda + k) * 4u));
         } else {
           const int kr = idx % BK, mr = idx / BK;
           const uint32_t m = bm0 + mr, k = k0 + kr;
-          sa1[j] = ld1(rsa, (m < p.M && k < p.K) ? (m * p.lda + k) * 4u : OOB);
+          sa1[j] = ld1(rsa, oob_unless((m < p.M) & (k < p.K), (m * p.lda + k) * 4u));
         }
       }
     }
@@ -260,19 +335,18 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
         if constexpr (BLD == B_KVEC) {
           const int kr = idx / (BN / 4), ncol = idx % (BN / 4);
           const uint32_t n = bn0 + 4 * ncol, k = k0 + kr;
-          sb4[j] = ld4(rsb, (n < p.N && k < p.K) ? (k * p.ldb + n) * 4u : OOB);
+          sb4[j] = ld4(rsb, oob_unless((n < p.N) & (k < p.K), (k * p.ldb + n) * 4u));
         } else if constexpr (BLD == B_KSCALAR) {
           const int kr = idx / BN, ncol = idx % BN;
           const uint32_t n = bn0 + ncol, k = k0 + kr;
-          sb1[j] = ld1(rsb, (n < p.N && k < p.K) ? (k * p.ldb + n) * 4u : OOB);
+          sb1[j] = ld1(rsb, oob_unless((n < p.N) & (k < p.K), (k * p.ldb + n) * 4u));
         } else {
           // this thread's k row; wave-uniform when BN is a multiple of 64
           uint32_t kr = (uint32_t)(idx / BN);
           if constexpr (BN % 64 == 0) kr = __builtin_amdgcn_readfirstlane(kr);
           const uint32_t k = k0 + kr;
           if constexpr (BLD == B_IM1X1) {
-            const bool ok = col_ok && k < p.K;
-            sb1[j] = ld1(rsb, ok ? (uint32_t)(col_base + (int)(k * p.HW)) * 4u : OOB);
+            sb1[j] = ld1(rsb, oob_unless(k < p.K, (uint32_t)(col_base + (int)(k * p.HW)) * 4u) | col_oob);
           } else {
             // k = (ic * KY + ky) * KX + kx
             const uint32_t ic = fdiv(k, p.kyx_m, p.kyx_s);
@@ -280,9 +354,9 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
             const uint32_t ky = fdiv(rem, p.kx_m, p.kx_s);
             const uint32_t kx = rem - ky * p.KX;
             const int iy = iy0 + (int)ky, ix = ix0 + (int)kx;
-            const bool ok = col_ok && k < p.K && (uint32_t)iy < p.H && (uint32_t)ix < p.W;
+            const bool ok = (k < p.K) & ((uint32_t)iy < p.H) & ((uint32_t)ix < p.W);
             const int off = col_base + (int)(ic * p.HW + ky * p.W + kx);
-            sb1[j] = ld1(rsb, ok ? (uint32_t)off * 4u : OOB);
+            sb1[j] = ld1(rsb, oob_unless(ok, (uint32_t)off * 4u) | col_oob);
           }
         }
       }
@@ -378,6 +452,7 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
   load_tiles(kbeg);
   store_tiles(0);
   __syncthreads();
+  KT(1);
   int buf = 0;
   for (uint32_t kt = 0; kt < nkt; ++kt) {
     const bool more = kt + 1 < nkt;
@@ -388,6 +463,7 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
     buf ^= 1;
   }
 
+  KT(2);
   // ---- epilogue
   const uint32_t n_base = bn0 + wn * WN + TN * li;
   if constexpr (SPLIT) {
@@ -434,10 +510,15 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
       *flag = last;
     }
     __syncthreads();
+    KT(3);
     if (!*flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
-    for (uint32_t c = tid; c < BM * BN / 4; c += NT)
-      combine_store<IM ? 1 : 0, true>(p, tile, tile_m, tile_n, c, gridDim.y, IM ? Lbias : nullptr);
+    combine_tile<IM ? 1 : 0, NT, BM * BN / 4 / NT, (BM * BN / 4 / NT < 4 ? BM * BN / 4 / NT : 4)>(
+        p, tile, tile_m, tile_n, gridDim.y, IM ? Lbias : nullptr, tid);
+#ifdef BH_KTRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KT(4);
+#endif
     return;
   }
   int cofs[TN];
@@ -486,6 +567,332 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
       }
     }
   }
+#ifdef BH_KTRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  KT(4);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Latency kernel for small ops (few output tiles, short K): the regime where a
+// call is a chain of memory round trips (~1 us each on a busy MI355X) rather
+// than MFMA work.
+//  * One block of 4 waves owns a small BM x BN tile and the waves split every
+//    64-deep K tile four ways (wave w takes k rows 16w..16w+15), so all four SIMDs
+//    work on one small tile and there are 4x more tiles than with one wave per
+//    32x32 subtile; the four partial tiles are summed through LDS at the end.
+//  * Operands go global -> LDS by LDS-DMA (buffer_load ... lds, per-lane source
+//    offsets, out-of-range lanes read as 0) into a ring of D stages with D-1 tiles
+//    in flight; one counted vmcnt + raw s_barrier per K tile (cdna_hip_programming.md
+//    §5 "Pipelining across barriers"), so a K step costs max(MFMA, latency / (D-1)).
+//  * 16-byte DMA wherever the layout allows (a dword DMA instruction costs about as
+//    much CU time as a 16-byte one): the m-major weight tile lands as [BM][64] with
+//    16-B chunk c of row m stored at c ^ (m & 15) (swizzled through the per-lane
+//    source address), so the b128 A-fragment reads of 16 consecutive rows hit
+//    distinct banks; 1x1 convs with OH*OW % 4 == 0 stream 4 pixels per lane.
+// Same GemmArgs contract, slab layout and split-K modes as gemm_kernel.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, 0, 0, 0);
+}
+
+template <int BM, int BN, int NW, int D, int ALD, int BLD, int SPL>
+__global__ __launch_bounds__(NW * 64) void gemm_sk_kernel(GemmArgs p) {
+  constexpr int NT = NW * 64, BK = 64, KW = BK / NW;  // KW: k rows per wave per stage
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int TM = BM / 32, TN = BN / 32;
+  static_assert(BM % 32 == 0 && BN % 32 == 0 && D >= 2, "sk tile shape");
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IM1X1 || BLD == B_IM1X1V);
+  constexpr bool AMM = (ALD == A_MVEC || ALD == A_MSCALAR);
+  // m-major A: 16-B DMA into swizzled [BM][64] (A_MVEC) or dword DMA into rows padded
+  // to 68 floats (A_MSCALAR: K % 4 != 0 or unaligned weights; one instruction per row)
+  constexpr int AST = ALD == A_MSCALAR ? BK + APAD : BK;
+  constexpr int A_LDS = AMM ? BM * AST : BK * BM;
+  constexpr int B_LDS = BK * BN;
+  constexpr int SLOT = A_LDS + B_LDS;
+  constexpr bool AV16 = (ALD == A_KVEC || ALD == A_MVEC);
+  constexpr bool BV16 = (BLD == B_KVEC || BLD == B_IM1X1V);
+  // LDS-DMA wave instructions per wave per stage (64 lanes x 16 or 4 bytes each)
+  constexpr int LA = AV16 ? BK * BM / (NW * 256) : BK * BM / (NW * 64);
+  constexpr int LB = BV16 ? BK * BN / (NW * 256) : BK * BN / (NW * 64);
+  static_assert(BK * BM % (NW * (AV16 ? 256 : 64)) == 0 && BK * BN % (NW * (BV16 ? 256 : 64)) == 0,
+                "whole DMA instructions per wave");
+  constexpr int LW = LA + LB;
+  static_assert(LA >= 1 && LB >= 1 && (D - 2) * LW <= 63, "vmcnt range");
+  constexpr int RED = NW * BM * BN;  // per-wave partial tiles, aliasing the ring after the loop
+  constexpr int SMF = D * SLOT > RED ? D * SLOT : RED;
+  constexpr int NCH = BM * BN / 4;           // float4 output chunks of the tile
+  constexpr int CH = (NCH + NT - 1) / NT;    // per thread
+  static_assert(NCH % NT == 0 || CH == 1, "sk epilogue chunking");
+  static_assert(BM <= 64, "bias arrives by one 64-lane DMA");
+
+  // one __shared__ array only (a second object makes hipcc wait vmcnt(0) at ds_reads)
+  __shared__ __attribute__((aligned(16))) float smem[SMF + 64 + 4];
+  float *const Lbias = smem + SMF;
+  uint32_t *const flag = (uint32_t *)(smem + SMF + 64);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  KT(0);
+  uint32_t tile_m, tile_n;
+  map_tile(blockIdx.x, p.tiles_m, p.tiles_n, tile_m, tile_n);
+  const uint32_t bm0 = tile_m * BM, bn0 = tile_n * BN;
+  constexpr bool SPLIT = SPL != 0;
+  const uint32_t split = SPLIT ? blockIdx.y : 0;
+  const uint32_t kbeg = split * p.ks;
+  const uint32_t kend = SPLIT ? min(p.K, kbeg + p.ks) : p.K;
+
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
+
+  // B DMA: this lane's column is fixed (64 % BN == 0); its k row within a stage is
+  // rb0 + j * (64 / BN) * NW... computed per instruction below
+  int col_base = 0, iy0 = 0, ix0 = 0;
+  uint32_t col_oob = 0;
+  if constexpr (IM) {
+    // this lane's (first) column is fixed: 64 % BN == 0 (dword), 64 % (BN / 4) == 0 (16 B)
+    const uint32_t col = bn0 + (uint32_t)(BLD == B_IM1X1V ? 4 * (lane % (BN / 4)) : lane % BN);
+    col_oob = col < p.N ? 0u : OOB;
+    const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
+    const uint32_t pix = col - img * p.OHW;
+    if constexpr (BLD == B_IM1X1) {
+      col_base = (int)(img * p.ICHW + pix);
+    } else {
+      const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s);
+      const uint32_t ox = pix - oy * p.OW;
+      iy0 = (int)(oy * p.sy) - (int)p.py;
+      ix0 = (int)(ox * p.sx) - (int)p.px;
+      col_base = (int)(img * p.ICHW) + iy0 * (int)p.W + ix0;
+    }
+  }
+
+  constexpr int RPI = BV16 ? 256 / BN : 64 / BN;  // B rows per DMA instruction
+  const uint32_t lr = (uint32_t)(BV16 ? lane / (BN / 4) : lane / BN);  // this lane's row in it
+  auto issue_stage = [&](int slot, uint32_t k0) {
+    float *const Ab = smem + slot * SLOT;
+    float *const Bb = Ab + A_LDS;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      const int ins = wave * LA + j;
+      if constexpr (ALD == A_MVEC) {
+        // 4 rows x 16 chunks per instruction; LDS chunk c of row m holds k chunk c ^ (m & 15)
+        const int r = 4 * ins + (lane >> 4), c = lane & 15;
+        const uint32_t m = bm0 + r, k = k0 + 4 * (c ^ (r & 15));
+        dma16(rsa, Ab + ins * 256, oob_unless((m < p.M) & (k < kend), (m * p.lda + k) * 4u));
+      } else if constexpr (ALD == A_MSCALAR) {
+        const uint32_t m = bm0 + ins, k = k0 + lane;
+        dma4(rsa, Ab + ins * AST, oob_unless((m < p.M) & (k < kend), (m * p.lda + k) * 4u));
+      } else {
+        constexpr int W = (ALD == A_KVEC) ? 4 : 1;
+        const int e = ins * 64 * W + W * lane;  // element index in [BK][BM]
+        const uint32_t m = bm0 + e % BM, k = k0 + e / BM;
+        const uint32_t off = oob_unless((m < p.M) & (k < kend), (k * p.lda + m) * 4u);
+        if constexpr (ALD == A_KVEC) dma16(rsa, Ab + ins * 256, off);
+        else dma4(rsa, Ab + ins * 64, off);
+      }
+    }
+    if constexpr (BLD == B_KVEC || BLD == B_KSCALAR) {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        constexpr int W = (BLD == B_KVEC) ? 4 : 1;
+        const int e = (wave * LB + j) * 64 * W + W * lane;  // element index in [BK][BN]
+        const uint32_t n = bn0 + e % BN, k = k0 + e / BN;
+        const uint32_t off = oob_unless((n < p.N) & (k < kend), (k * p.ldb + n) * 4u);
+        if constexpr (BLD == B_KVEC) dma16(rsb, Bb + (wave * LB + j) * 256, off);
+        else dma4(rsb, Bb + (wave * LB + j) * 64, off);
+      }
+    } else if constexpr (BLD == B_IM1X1 || BLD == B_IM1X1V) {
+      // k = k0 + RPI*i + lr with i = wave*LB + j: offset linear in i
+      const uint32_t vb = (uint32_t)(col_base + (int)((k0 + lr + RPI * wave * LB) * p.HW)) * 4u;
+      const int kl = (int)kend - (int)(k0 + lr + RPI * wave * LB);
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const uint32_t off = oob_unless(RPI * j < kl, vb + RPI * j * p.HW * 4u) | col_oob;
+        if constexpr (BLD == B_IM1X1V) dma16(rsb, Bb + (wave * LB + j) * 256, off);
+        else dma4(rsb, Bb + (wave * LB + j) * 64, off);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        // (ic, ky, kx) of the instruction's first row (wave-uniform, scalar), then this lane's row
+        const uint32_t k1 = k0 + RPI * (wave * LB + j);
+        uint32_t ic = fdiv(k1, p.kyx_m, p.kyx_s);
+        const uint32_t rem = k1 - ic * p.KYX;
+        uint32_t ky = fdiv(rem, p.kx_m, p.kx_s);
+        uint32_t kx = rem - ky * p.KX;
+        if constexpr (RPI > 1) {
+          kx += lr;  // lr < RPI <= 2 and KX >= 1: at most one carry per level
+          if (kx >= p.KX) { kx -= p.KX; ++ky; }
+          if (ky * p.KX >= p.KYX) { ky = 0; ++ic; }  // ky == KY
+        }
+        const uint32_t k = k1 + lr;
+        const int iy = iy0 + (int)ky, ix = ix0 + (int)kx;
+        const bool ok = (k < kend) & ((uint32_t)iy < p.H) & ((uint32_t)ix < p.W);
+        dma4(rsb, Bb + (wave * LB + j) * 64,
+             oob_unless(ok, (uint32_t)(col_base + (int)(ic * p.HW + ky * p.W + kx)) * 4u) | col_oob);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  const int kh = lane >> 5, li = lane & 31;
+  // wave w owns k rows KW*w .. KW*w+KW-1 of a stage; lane half h the KW/2 rows from
+  // KW*w + h*KW/2 (the same k for A and B)
+  auto compute = [&](int slot) {
+    const float *const Ab = smem + slot * SLOT;
+    const float *const Bb = Ab + A_LDS + TN * li;
+#pragma unroll
+    for (int kq = 0; kq < KW / 8; ++kq) {
+      const int cc = (KW * wave + kh * (KW / 2)) / 4 + kq;  // 16-B k chunk of the A rows
+      f32x4v am[AMM ? TM : 1];
+      if constexpr (AMM) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          const int m = TM * li + t;
+          am[t] = *(const f32x4v *)&Ab[ALD == A_MVEC ? m * AST + 4 * (cc ^ (m & 15)) : m * AST + 4 * cc];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int krow = 4 * cc + q;
+        float a[TM], b[TN];
+        if constexpr (AMM) {
+#pragma unroll
+          for (int t = 0; t < TM; ++t) a[t] = am[t][q];
+        } else {
+          typename fvec<TM>::t av = *(const typename fvec<TM>::t *)&Ab[krow * BM + TM * li];
+#pragma unroll
+          for (int t = 0; t < TM; ++t) a[t] = vget<TM>(av, t);
+        }
+        typename fvec<TN>::t bv = *(const typename fvec<TN>::t *)&Bb[krow * BN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = vget<TN>(bv, j);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- main loop: D-stage LDS-DMA ring, D-1 K tiles in flight
+  const uint32_t nkt = (kend - kbeg + BK - 1) / BK;
+  if constexpr (IM && SPL != 1) {
+    // biases by one DMA of wave 0, issued before stage 0 so the first stage wait covers it
+    const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+    if (wave == 0) dma4(rsbias, Lbias, oob_unless((lane < BM) & (bm0 + lane < p.M), (bm0 + lane) * 4u));
+  }
+  // Stages past the split's end are issued too (their lanes read OOB zeros without
+  // touching memory), so every wave always has exactly D-2 stages in flight behind
+  // the one it waits for and the issue code has no branches (it interleaves with
+  // the MFMAs); the ring is drained before the LDS is reused below.
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) issue_stage(s, kbeg + s * BK);
+  int slot = 0;
+  for (uint32_t kt = 0; kt < nkt; ++kt) {
+    vm_wait<(D - 2) * LW>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt landed for all waves; all done reading kt-1
+    asm volatile("" ::: "memory");
+    if (kt == 0) KT(1);
+    issue_stage(slot == 0 ? D - 1 : slot - 1, kbeg + (kt + D - 1) * BK);  // slot (kt-1) % D
+    compute(slot);
+    slot = slot == D - 1 ? 0 : slot + 1;
+  }
+  vm_wait<0>();
+  KT(2);
+
+  // ---- sum the four waves' partial tiles through LDS (row-major BM x BN per wave)
+  __syncthreads();  // every wave is done reading the ring; no DMA is in flight
+  {
+    float *const Rw = smem + wave * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+        typename fvec<TN>::t w;
+        if constexpr (TN == 1) w = acc[i][0][r]; else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
+        }
+        *(typename fvec<TN>::t *)&Rw[row * BN + TN * li] = w;
+      }
+  }
+  __syncthreads();
+  const bool has_chunk = NCH % NT == 0 || tid < NCH;
+  f32x4v v[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int c = has_chunk ? tid + j * NT : 0;
+    v[j] = *(const f32x4v *)&smem[4 * c];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v[j] += *(const f32x4v *)&smem[w * BM * BN + 4 * c];
+  }
+  if constexpr (!SPLIT) {
+    if (has_chunk) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        finish_store<IM ? 1 : 0>(p, tile_m, tile_n, tid + j * NT, v[j], IM ? Lbias : nullptr);
+    }
+#ifdef BH_KTRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KT(4);
+#endif
+    return;
+  } else {
+    const uint32_t tile = tile_m * p.tiles_n + tile_n;
+    const size_t slab_off = ((size_t)split * p.tiles_m * p.tiles_n + tile) * (BM * BN);
+    float *const wz = p.ws + slab_off;
+    if constexpr (SPL == 1) {
+      if (has_chunk) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) *(f32x4v *)&wz[4 * (tid + j * NT)] = v[j];
+      }
+      return;
+    } else {
+      const __amdgpu_buffer_rsrc_t rw = make_rsrc(wz, BM * BN * 4);
+      if (has_chunk) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]), rw, 16 * (tid + j * NT), 0,
+              AUX_SC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
+        if (last) __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
+      __syncthreads();
+      KT(3);
+      if (!*flag) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+      combine_tile<IM ? 1 : 0, NT, CH, CH, NCH>(p, tile, tile_m, tile_n, gridDim.y, IM ? Lbias : nullptr, tid);
+#ifdef BH_KTRACE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      KT(4);
+#endif
+    }
+  }
 }
 
 // Split-K combine pass (SPL == 1): one thread per float4 chunk of every tile.
@@ -496,7 +903,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs p, uint32_t
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t tile = (uint32_t)(e / per_tile), c = (uint32_t)(e - (uint64_t)tile * per_tile);
     const uint32_t tile_m = tile / p.tiles_n, tile_n = tile - tile_m * p.tiles_n;
-    combine_store<IMODE, false>(p, tile, tile_m, tile_n, c, S, nullptr);
+    combine_store<IMODE>(p, tile, tile_m, tile_n, c, S, nullptr);
   }
 }
 
@@ -509,7 +916,7 @@ typedef void (*kern_t)(GemmArgs);
 struct cfg_t {
   const char *name;
   int BM, BN, BK, NT;
-  kern_t k[4][4][3];  // [A loader][B loader][SPL]
+  kern_t k[4][5][3];  // [A loader][B loader][SPL]
 };
 
 template <int BM, int BN, int BK, int TM, int TN, int WM_, int WN_, int ALD, int BLD>
@@ -517,6 +924,30 @@ void reg_kernels(cfg_t &c) {
   c.k[ALD][BLD][0] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 0>;
   c.k[ALD][BLD][1] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 1>;
   c.k[ALD][BLD][2] = gemm_kernel<BM, BN, BK, TM, TN, WM_, WN_, ALD, BLD, 2>;
+}
+template <int BM, int BN, int NW, int D, int ALD, int BLD>
+void reg_sk_kernels(cfg_t &c) {
+  c.k[ALD][BLD][0] = gemm_sk_kernel<BM, BN, NW, D, ALD, BLD, 0>;
+  c.k[ALD][BLD][1] = gemm_sk_kernel<BM, BN, NW, D, ALD, BLD, 1>;
+  c.k[ALD][BLD][2] = gemm_sk_kernel<BM, BN, NW, D, ALD, BLD, 2>;
+}
+template <int BM, int BN, int NW, int D>
+cfg_t conv_sk_cfg(const char *name) {
+  cfg_t c{name, BM, BN, 64, NW * 64, {}};
+  reg_sk_kernels<BM, BN, NW, D, A_MVEC, B_IM2COL>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_MSCALAR, B_IM2COL>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_MVEC, B_IM1X1>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_MSCALAR, B_IM1X1>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_MVEC, B_IM1X1V>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_MSCALAR, B_IM1X1V>(c);
+  return c;
+}
+template <int BM, int BN, int NW, int D>
+cfg_t sgemm_sk_cfg(const char *name) {
+  cfg_t c{name, BM, BN, 64, NW * 64, {}};
+  reg_sk_kernels<BM, BN, NW, D, A_KVEC, B_KVEC>(c);
+  reg_sk_kernels<BM, BN, NW, D, A_KSCALAR, B_KSCALAR>(c);
+  return c;
 }
 template <int BM, int BN, int BK, int TM, int TN, int WM_, int WN_>
 cfg_t conv_cfg(const char *name) {
@@ -543,6 +974,10 @@ const std::vector<cfg_t> &cfgs(int op) {
       sgemm_cfg<256, 128, 16, 4, 2, 2, 2>("256x128x16"),
       sgemm_cfg<128, 64, 16, 2, 1, 2, 2>("128x64x16"),
       sgemm_cfg<64, 64, 16, 1, 1, 2, 2>("64x64x16"),
+      sgemm_sk_cfg<32, 32, 4, 4>("sk32x32x64"),
+      sgemm_sk_cfg<64, 64, 4, 3>("sk64x64x64"),
+      sgemm_sk_cfg<32, 32, 8, 4>("sk32x32x64w8"),
+      sgemm_sk_cfg<64, 64, 8, 4>("sk64x64x64w8"),
   };
   static const std::vector<cfg_t> cv = {
       conv_cfg<128, 128, 32, 2, 2, 2, 2>("128x128x32"),
@@ -554,6 +989,13 @@ const std::vector<cfg_t> &cfgs(int op) {
       conv_cfg<128, 32, 32, 1, 1, 4, 1>("128x32x32"),
       conv_cfg<256, 128, 16, 4, 2, 2, 2>("256x128x16"),
       conv_cfg<64, 32, 32, 1, 1, 2, 1>("64x32x32"),
+      conv_sk_cfg<32, 32, 4, 4>("sk32x32x64"),
+      conv_sk_cfg<32, 64, 4, 4>("sk32x64x64"),
+      conv_sk_cfg<64, 32, 4, 4>("sk64x32x64"),
+      conv_sk_cfg<64, 64, 4, 3>("sk64x64x64"),
+      conv_sk_cfg<32, 32, 8, 4>("sk32x32x64w8"),
+      conv_sk_cfg<32, 64, 8, 4>("sk32x64x64w8"),
+      conv_sk_cfg<64, 64, 8, 4>("sk64x64x64w8"),
   };
   return op == 0 ? sg : cv;
 }
@@ -712,6 +1154,9 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   cfg_t const &c = cfgs(op)[ch.cfg];
   p.tiles_m = (p.M + c.BM - 1) / c.BM;
   p.tiles_n = (p.N + c.BN - 1) / c.BN;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
   const uint64_t nblk = (uint64_t)p.tiles_m * p.tiles_n;
   if (nblk > 0x7fffffffu) return bh::fail(BH_UNSUP, std::string(what) + ": grid too large");
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
@@ -722,12 +1167,13 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   // fully parallel reduce pass is cheaper than serial combining by last arrivers)
   int red = S <= 1 ? 0 : (ch.red ? ch.red : (nblk >= 64 || S > 4 ? 1 : 2));
   if (red == 2 && (uint64_t)S * nblk * c.BM * c.BN * 4 >= 0x7fffff00ull) red = 1;  // sc1 offsets are 32-bit
+  if (bld == B_IM1X1V && !c.k[ald][bld][red]) bld = B_IM1X1;  // tile kernels: no 4-pixel loader
   kern_t k = c.k[ald][bld][red];
   if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
   void *args[] = {&p};
+  p.tbm = c.BM;
+  p.tbn = c.BN;
   if (S > 1) {
-    p.tbm = c.BM;
-    p.tbn = c.BN;
     int rc = ensure_ws(ctx, (size_t)S * nblk * c.BM * c.BN * 4);
     if (rc != BH_OK) return rc;
     p.ws = (float *)ctx->ws;
@@ -741,7 +1187,7 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
     if (rc != BH_OK) return rc;
     const uint64_t total = nblk * c.BM * c.BN / 4;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
-    const void *rk = (bld == B_IM2COL || bld == B_IM1X1) ? (const void *)splitk_reduce_kernel<1>
+    const void *rk = (bld == B_IM2COL || bld == B_IM1X1 || bld == B_IM1X1V) ? (const void *)splitk_reduce_kernel<1>
                                                           : (const void *)splitk_reduce_kernel<0>;
     uint32_t Sv = S;
     void *rargs[] = {&p, &Sv};
@@ -841,7 +1287,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *b
   p.a_bytes = (uint32_t)w_bytes;
   p.b_bytes = (uint32_t)in_bytes;
   p.relu = relu;
-  p.cvec = 0;
+  p.cvec = (OH * OW) % 4 == 0 && ((uintptr_t)out % 16 == 0);  // output rows take float4 stores
   p.H = H; p.W = W; p.KX = KX; p.KYX = KY * KX;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px;
   p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = OC * OH * OW;
@@ -850,10 +1296,11 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *b
   set_fd(p.OHW, p.ohw_m, p.ohw_s);
   set_fd(OW, p.ow_m, p.ow_s);
   const bool k1 = KY == 1 && KX == 1 && sy == 1 && sx == 1 && py == 0 && px == 0;
+  const bool k1v = k1 && (H * W) % 4 == 0 && ((uintptr_t)in % 16 == 0);
   const bool avec = (K % 4 == 0) && ((uintptr_t)filts % 16 == 0);
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
-  return launch_gemm(ctx, 1, ch, avec ? A_MVEC : A_MSCALAR, k1 ? B_IM1X1 : B_IM2COL, p, "conv");
+  return launch_gemm(ctx, 1, ch, avec ? A_MVEC : A_MSCALAR, k1v ? B_IM1X1V : (k1 ? B_IM1X1 : B_IM2COL), p, "conv");
 }
 
 }  // namespace bh

@@ -19,6 +19,11 @@ thread_local std::string g_last_error;
 __global__ void stamp_kernel(unsigned long long *t, int slot) {
   if (threadIdx.x == 0) t[slot] = wall_clock64();
 }
+// bounded busy-wait on the 100 MHz constant clock (every wave exits after us µs)
+__global__ void spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
 constexpr int STAMP_SLOTS = 1 << 18;
 }
 
@@ -258,6 +263,15 @@ int bh_stamp(bh_ctx *c, int slot) {
   void *args[] = {&t, &slot};
   BH_HIP(hipLaunchKernel((const void *)stamp_kernel, dim3(1), dim3(64), args, 0, c->stream));
   return bh::check_launch("stamp");
+}
+
+int bh_spin(bh_ctx *c, int us) {
+  BH_CHECK_CTX(c);
+  if (us < 1 || us > 100000) return bh::fail(BH_ERR, "bh_spin: us out of range 1..100000");
+  unsigned long long ticks = (unsigned long long)us * (unsigned long long)(c->stamp_hz / 1e6);
+  void *args[] = {&ticks};
+  BH_HIP(hipLaunchKernel((const void *)spin_kernel, dim3(1), dim3(64), args, 0, c->stream));
+  return bh::check_launch("spin");
 }
 
 int bh_stamps_read(bh_ctx *c, int first, int n, double *us) {

@@ -82,6 +82,10 @@ int bh_time_next_call(bh_ctx *ctx, int *begin_id, int *end_id);
  * relative to slot first. */
 int bh_stamp(bh_ctx *ctx, int slot);
 int bh_stamps_read(bh_ctx *ctx, int first, int n, double *us);
+/* enqueue a one-block kernel that busy-waits us microseconds (1..100000) on the
+ * device clock: queued work behind it starts back to back, so events recorded
+ * around a batch measure GPU time, not host launch latency. */
+int bh_spin(bh_ctx *ctx, int us);
 
 /* ---- launch batching: capture everything issued on the context between
  *      begin and end (kernels, event records) into a hipGraph and replay it

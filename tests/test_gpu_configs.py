@@ -21,6 +21,9 @@ CONV_SHAPES = [
     ops.ConvShape(3, 5, 9, 13, 37, 3, 3, 2, 1, 1, 0),    # im2col, K = 45 (A scalar), stride 2
     ops.ConvShape(2, 132, 7, 5, 150, 1, 1, 1, 1, 0, 0),  # 1x1, K = 132
     ops.ConvShape(1, 17, 6, 6, 33, 1, 1, 1, 1, 0, 0),    # 1x1, K = 17 (A scalar)
+    ops.ConvShape(2, 40, 8, 8, 20, 1, 1, 1, 1, 0, 0),    # 1x1, OH*OW % 4 == 0 (float4 output rows)
+    ops.ConvShape(1, 8, 6, 6, 48, 3, 3, 1, 1, 1, 1),     # im2col, OH*OW % 4 == 0
+    ops.ConvShape(1, 520, 4, 4, 40, 1, 1, 1, 1, 0, 0),   # 1x1, long K (register ring wraps)
 ]
 
 

@@ -4,14 +4,16 @@
 The backend's counterpart of Boda's op_tune sweeps + wisdom (src/rtc_prof.cc
 ops-prof over several --op-tunes; src/op-tuner.cc): for every op of the given
 op lists, time each instantiated tile configuration with each split count
-(median over --reps calls, each after a cache flush, timed by events on the
-call's own kernel dispatches), keep the fastest and
+(amortized over a replayed graph of back-to-back calls, as bench.py reports
+per-op time; --timing flush: median over --reps calls, each after a cache flush,
+timed by events on the call's own kernel dispatches), keep the fastest and
 write boda-1_amd/tuning/gfx950.tune lines "<op> <dims> cfg=<name> splits=<n>".
 Results of every candidate go to --json for analysis.
 
   python tools/tune.py --sets conv,sgemm-full --out boda-1_amd/tuning/gfx950.tune
 """
 import argparse
+import re
 import json
 import os
 import statistics
@@ -34,13 +36,35 @@ CFG_BK = {}
 
 
 def bk_of(name):
-    return int(name.split("x")[2])
+    """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
+    return int(re.match(r"\d+", name.split("x")[2]).group(0))
 
 
 FLUSH = None
 
 
+TIMING = "graph"
+
+
 def time_op(dev, wl, i, reps):
+    """GPU ms per call in the regime the bench reports (TIMING "graph"): amortized over a
+    replayed hipGraph of back-to-back calls (runner.op_graph_time). TIMING "flush": see
+    time_op_flush."""
+    if TIMING == "flush":
+        return time_op_flush(dev, wl, i, reps)
+    wl.launch(i)  # warm-up (grows the split-K workspace)
+    b, e = dev.time_next_call()
+    wl.launch(i)
+    dev.sync()
+    est = dev.elapsed_ms(b, e) * 1e-3
+    dev.events_reset()
+    n = max(3, min(100, int(round(1e-3 / max(est, 1e-6)))))
+    t = min(wl.op_graph_time(i, n) for _ in range(2))
+    dev.events_reset()
+    return t * 1e3
+
+
+def time_op_flush(dev, wl, i, reps):
     """Median GPU time of one call (ms) as the bench sees it: each launch preceded by a
     512 MiB memset that evicts L2 and the Infinity Cache (in the bench every op runs after
     220 others), timed by events on the call's own kernel dispatches."""
@@ -60,17 +84,17 @@ def time_op(dev, wl, i, reps):
     return statistics.median(out)
 
 
-FLUSH = None
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default="conv,sgemm-full,sgemm-small")
     ap.add_argument("--out", default=os.path.join(ROOT, "boda-1_amd", "tuning", "gfx950.tune"))
     ap.add_argument("--json", default="")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--timing", choices=["graph", "flush"], default="graph")
     ap.add_argument("--max-flop-sgemm", type=float, default=3e12, help="skip sgemm sweeps above this (use heuristic)")
     args = ap.parse_args()
+    global TIMING
+    TIMING = args.timing
 
     dev = boda_hip.Device(0)
     plat = dev.plat_tag()
