@@ -25,7 +25,8 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
            "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
-           "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin"]
+           "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
+           "bh_conv_filts_packed_floats", "bh_conv_filts_pack"]
 
 
 class BodaHipError(RuntimeError):
@@ -69,6 +70,10 @@ def lib():
         L.bh_gen_data.argtypes = [c_vp, ctypes.c_int, c_vp, ctypes.POINTER(c_u32), c_u32, ctypes.c_float]
         L.bh_sgemm_kmajor.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32]
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
+        L.bh_conv2d_fwd_nchw_pk.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
+        L.bh_conv_filts_packed_floats.argtypes = [c_u32] * 4
+        L.bh_conv_filts_packed_floats.restype = ctypes.c_size_t
+        L.bh_conv_filts_pack.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 4
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
         L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
         L.bh_spin.argtypes = [c_vp, ctypes.c_int]
@@ -101,6 +106,11 @@ def variant_name(op_kind, dims):
     buf = ctypes.create_string_buffer(256)
     _check(lib().bh_variant_name(op_kind, arr, buf, 256))
     return buf.value.decode()
+
+
+def conv_filts_packed_floats(s):
+    """Floats of the transformed filter bank (bh_conv_filts_pack) for conv shape s."""
+    return lib().bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX)
 
 
 def tune_cfg_names(op_kind):
@@ -241,7 +251,16 @@ class Device:
     def sgemm(self, a, b, c, M, N, K):
         _check(lib().bh_sgemm_kmajor(self.ctx, a.ptr, b.ptr, c.ptr, M, N, K))
 
-    def conv(self, inp, filts, biases, out, s, relu=1):
-        _check(lib().bh_conv2d_fwd_nchw(self.ctx, inp.ptr, filts.ptr, biases.ptr if biases is not None else None,
-                                        out.ptr, s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px,
-                                        int(relu)))
+    def conv(self, inp, filts, biases, out, s, relu=1, packed=None):
+        """bh_conv2d_fwd_nchw; with packed (a bank made by conv_filts_pack) bh_conv2d_fwd_nchw_pk."""
+        bp = biases.ptr if biases is not None else None
+        if packed is None:
+            _check(lib().bh_conv2d_fwd_nchw(self.ctx, inp.ptr, filts.ptr, bp, out.ptr, s.B, s.IC, s.H, s.W, s.OC,
+                                            s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu)))
+        else:
+            _check(lib().bh_conv2d_fwd_nchw_pk(self.ctx, inp.ptr, filts.ptr, packed.ptr, bp, out.ptr, s.B, s.IC, s.H,
+                                               s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu)))
+
+    def conv_filts_pack(self, filts, packed, s):
+        """Boda's xpose_filts counterpart: write the k-major bank of filts into packed."""
+        _check(lib().bh_conv_filts_pack(self.ctx, filts.ptr, packed.ptr, s.OC, s.IC, s.KY, s.KX))

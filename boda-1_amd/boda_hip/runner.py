@@ -5,13 +5,15 @@ For each op: create its vars on the device (zero-filled), fill the inputs with
 the reference's gen_data (mode 5 by default) on the device, then launch the
 main kernel as often as asked, timing each launch between a pair of HIP
 events on the context's stream (the reference times exactly this: one
-main-kernel call, no data generation or layout transforms, F7). A step can be
+main-kernel call, no data generation or layout transforms, F7: the filter-bank
+transform the k-major conv kernels read is made once per op at setup, like the
+reference's xpose_filts). A step can be
 captured into a hipGraph and replayed, so the GPU runs the op sweep back to
 back instead of waiting on per-launch host latency.
 """
 from dataclasses import dataclass
 
-from . import GEN_CONV_BIASES, GEN_CONV_FILTS, GEN_CONV_IN, GEN_SGEMM_A, GEN_SGEMM_B
+from . import GEN_CONV_BIASES, GEN_CONV_FILTS, GEN_CONV_IN, GEN_SGEMM_A, GEN_SGEMM_B, conv_filts_packed_floats
 from .ops import ConvShape, SgemmShape
 
 # MI355X peaks (MI355X_MICROARCH.md): fp32 matrix = vector = 157.3 TFLOP/s; HBM3E 8.0 TB/s.
@@ -36,7 +38,7 @@ class OpVars:
 
 
 class Workload:
-    def __init__(self, dev, shapes, mode=5, tags=None):
+    def __init__(self, dev, shapes, mode=5, tags=None, pack=True):
         self.dev = dev
         self.ops = []
         for i, s in enumerate(shapes):
@@ -56,7 +58,13 @@ class Workload:
                 dev.gen_data(GEN_CONV_IN, inp, [s.B, s.IC, s.H, s.W], mode)
                 dev.gen_data(GEN_CONV_FILTS, f, [s.OC, s.IC, s.KY, s.KX], mode)
                 dev.gen_data(GEN_CONV_BIASES, bi, [s.OC], mode)
-                self.ops.append(OpVars(s, (inp, f, bi, o), tag))
+                # the filter-bank transform, once per op before any timed call, as the
+                # reference's xpose_filts (src/rtc_prof.cc:93-99; untimed, F7)
+                pk = None
+                if pack:
+                    pk = dev.alloc_floats(conv_filts_packed_floats(s))
+                    dev.conv_filts_pack(f, pk, s)
+                self.ops.append(OpVars(s, (inp, f, bi, pk, o), tag))
             else:
                 raise TypeError(s)
         dev.sync()
@@ -68,8 +76,8 @@ class Workload:
             a, b, c = v.bufs
             self.dev.sgemm(a, b, c, s.M, s.N, s.K)
         else:
-            inp, f, bi, o = v.bufs
-            self.dev.conv(inp, f, bi, o, s, 1)
+            inp, f, bi, pk, o = v.bufs
+            self.dev.conv(inp, f, bi, o, s, 1, packed=pk)
 
     def output(self, i):
         return self.ops[i].bufs[-1].download()
@@ -136,5 +144,6 @@ class Workload:
     def free(self):
         for v in self.ops:
             for b in v.bufs:
-                b.free()
+                if b is not None:
+                    b.free()
         self.ops = []

@@ -29,6 +29,8 @@ struct bh_ctx {
   double stamp_hz = 100e6;
   void *cnt = nullptr;  // split-K arrival tickets
   uint64_t cnt_n = 0;
+  void *wpack = nullptr;  // k-major filter bank for the ring conv kernels, grown on demand
+  size_t wpack_bytes = 0;
 };
 
 namespace bh {
@@ -74,9 +76,12 @@ inline fastdiv make_fastdiv(uint32_t d) {
 namespace bh {
 int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi);
 int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t M, uint32_t N, uint32_t K);
-int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *biases, float *out,
-                uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
-                uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu);
+int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
+                float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+                uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu);
+size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
+int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
+                           uint32_t KX);
 std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
 std::string conv_variant(const uint32_t *d);
 int tune_set(bh_ctx *ctx, int op, int cfg, int splits);

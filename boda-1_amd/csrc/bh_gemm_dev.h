@@ -1,0 +1,244 @@
+// bh_gemm_dev.h -- device-side building blocks shared by the GEMM / conv kernel sources
+// (bh_gemm.hip: register-staged tile kernels + latency kernels; bh_ring.hip: LDS-DMA ring
+// kernels). Internal to libboda_hip.so.
+#pragma once
+#include "bh_common.h"
+
+namespace bhk {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
+enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5 };
+// B_IMT2: ring kernels' im2col when IC >= BK: a wave's rows of one K tile touch at most two
+// filter taps (ring kernels read K in (ky, kx, ic) order)
+// B_IM1X1V: 1x1 conv whose OH*OW % 4 == 0 with a 16-B aligned input: four adjacent output
+// columns are four adjacent input pixels of one image (latency kernel only; the tile
+// kernel treats it as B_IM1X1)
+
+constexpr uint32_t OOB = 0x80000000u;  // buffer offset that always misses (extents < 2^31)
+constexpr int APAD = 4;                // m-major A tile row padding (floats)
+
+struct GemmArgs {
+  const float *a, *b;
+  float *c;
+  const float *bias;
+  float *ws;       // split-K partial slabs, tile-major: [S][tile][BM*BN]
+  uint32_t *cnt;   // split-K arrival tickets, one per tile (zero between calls)
+  uint32_t M, N, K;
+  uint32_t lda, ldb, ldc;
+  uint32_t tbm, tbn;          // tile shape (for the split-K combine)
+  uint32_t ks;                // K extent of one split (multiple of BK)
+  uint32_t a_bytes, b_bytes;  // buffer extents in bytes (reads beyond come back 0)
+  uint32_t tiles_m, tiles_n;
+  int relu;
+  int cvec;  // dense C rows can take TN-wide vector stores
+  // implicit im2col (B_IM2COL / B_IM1X1); N = B*OH*OW, K = IC*KY*KX
+  uint32_t H, W, KX, KYX, sy, sx, py, px, OW, OHW, HW, ICHW, OCOHW;
+  uint32_t kyx_m, kyx_s, kx_m, kx_s, ohw_m, ohw_s, ow_m, ow_s;  // fastdiv constants
+  uint32_t IC, ic_m, ic_s;  // ring kernels: K order (ky, kx, ic) of the repacked filter bank
+#ifdef BH_KTRACE
+  unsigned long long *trace;  // per-block device-clock marks (tools/ktrace.py)
+#endif
+};
+
+#ifdef BH_KTRACE
+#define KT(k)                                                                                     \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      p.trace[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = wall_clock64();          \
+  } while (0)
+#else
+#define KT(k) \
+  do {        \
+  } while (0)
+#endif
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) {
+  return (__umulhi(n, m) + n) >> s;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+// Offset, or the always-missing OOB offset when !ok. Callers combine conditions with
+// bitwise & (no short-circuit): a && chain lets hipcc turn the select into a branch
+// around each load, which also breaks its vmcnt bookkeeping for the ring.
+__device__ __forceinline__ uint32_t oob_unless(bool ok, uint32_t off) { return ok ? off : OOB; }
+__device__ __forceinline__ f32x4v ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+__device__ __forceinline__ void map_tile(uint32_t bid, uint32_t tiles_m, uint32_t tiles_n, uint32_t &tm,
+                                         uint32_t &tn) {
+  uint32_t nwg = tiles_m * tiles_n;
+  uint32_t xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const uint32_t G = 8;
+  uint32_t per_group = G * tiles_n;
+  uint32_t group = wgid / per_group;
+  uint32_t first_m = group * G;
+  uint32_t gsm = min(tiles_m - first_m, G);
+  uint32_t rem = wgid - group * per_group;
+  tm = first_m + rem % gsm;
+  tn = rem / gsm;
+}
+
+template <int N>
+struct fvec;
+template <>
+struct fvec<1> { typedef float t; };
+template <>
+struct fvec<2> { typedef f32x2v t; };
+template <>
+struct fvec<4> { typedef f32x4v t; };
+
+template <int N>
+__device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
+  if constexpr (N == 1) return v;
+  else return v[i];
+}
+
+// Split-K slabs are summed in fixed order s = 0..S-1 (bitwise reproducible whoever
+// combines: the reduce kernel or a tile's last-arriving block).
+// Bias, ReLU and store of one float4 chunk c (tile elements 4c..4c+3, row-major BM x BN)
+// of tile (tile_m, tile_n): dense C rows, or NCHW scatter for conv (IMODE). p.cvec: rows
+// take aligned float4 stores (dense: ldc % 4 == 0; conv: OH*OW % 4 == 0).
+template <int IMODE>
+__device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
+                                             f32x4v sum, const float *bias_lds) {
+  const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
+  const uint32_t m = tile_m * p.tbm + row;
+  if (m >= p.M) return;
+  const float b = bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f);
+  const uint32_t n0 = tile_n * p.tbn + col0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float x = sum[t] + b;
+    sum[t] = (p.relu && x < 0.0f) ? 0.0f : x;
+  }
+  if (p.cvec && n0 + 4 <= p.N) {
+    size_t o;
+    if constexpr (IMODE) {
+      const uint32_t img = fdiv(n0, p.ohw_m, p.ohw_s);
+      o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n0 - img * p.OHW);
+    } else {
+      o = (size_t)m * p.ldc + n0;
+    }
+    *(f32x4v *)&p.c[o] = sum;
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t n = n0 + t;
+    if (n >= p.N) break;
+    if constexpr (IMODE) {
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW)] = sum[t];
+    } else {
+      p.c[(size_t)m * p.ldc + n] = sum[t];
+    }
+  }
+}
+
+constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
+
+// Split-K combine of one float4 chunk c for the reduce kernel (after a kernel boundary,
+// so plain loads): the S slabs summed in fixed order, four in flight.
+template <int IMODE>
+__device__ __forceinline__ void combine_store(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
+                                              uint32_t c, uint32_t S, const float *bias_lds) {
+  const size_t tsz = (size_t)p.tbm * p.tbn, slab = tsz * p.tiles_m * p.tiles_n;
+  f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t q = 0;
+  const f32x4v *src = (const f32x4v *)(p.ws + (size_t)tile * tsz) + c;
+  for (; q + 4 <= S; q += 4) {
+    f32x4v a0 = src[(q + 0) * slab / 4], a1 = src[(q + 1) * slab / 4];
+    f32x4v a2 = src[(q + 2) * slab / 4], a3 = src[(q + 3) * slab / 4];
+    sum += a0; sum += a1; sum += a2; sum += a3;
+  }
+  for (; q < S; ++q) sum += src[q * slab / 4];
+  finish_store<IMODE>(p, tile_m, tile_n, c, sum, bias_lds);
+}
+
+// In-kernel split-K combine of a whole tile by one block (the last arriver): each
+// thread owns CH float4 chunks (c = tid + j*NT), processed G at a time with all of
+// a group's loads for two slabs issued before any is consumed, so the slab reads
+// overlap instead of costing one L2 round trip per chunk. Same fixed slab order as
+// combine_store (bitwise identical results).
+template <int IMODE, int NT, int CH, int G, int NCH = CH * NT>
+__device__ __forceinline__ void combine_tile(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
+                                             uint32_t S, const float *bias_lds, int tid) {
+  static_assert(CH % G == 0, "chunk grouping");
+  if (NCH % NT != 0 && tid >= NCH) return;  // fewer chunks than threads (CH == 1)
+  const uint32_t tsz = p.tbm * p.tbn, sstep = tsz * p.tiles_m * p.tiles_n * 4;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws, 0x7fffff00u);
+#pragma unroll 1
+  for (int g = 0; g < CH; g += G) {
+    uint32_t off[G];
+    f32x4v sum[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      off[j] = (tile * tsz + 4 * (uint32_t)(tid + (g + j) * NT)) * 4;
+      sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    uint32_t q = 0;
+    for (; q + 2 <= S; q += 2) {
+      f32x4v x0[G], x1[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        x0[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
+        x1[j] = __builtin_bit_cast(f32x4v,
+                                   __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + (q + 1) * sstep, 0, AUX_SC1));
+      }
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        sum[j] += x0[j];
+        sum[j] += x1[j];
+      }
+    }
+    if (q < S) {
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        sum[j] += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) finish_store<IMODE>(p, tile_m, tile_n, (uint32_t)(tid + (g + j) * NT), sum[j], bias_lds);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, 0, 0, 0);
+}
+
+
+typedef void (*kern_t)(GemmArgs);
+
+struct cfg_t {
+  const char *name;
+  int BM, BN, BK, NT;
+  kern_t k[4][6][3];  // [A loader][B loader][SPL]
+  int packA;          // conv: A is the filter bank repacked k-major [K][OC4] (bh_ring.hip)
+};
+
+// bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and
+// the repack itself (into the context's wpack buffer; first dispatch of a conv call)
+std::vector<cfg_t> ring_cfgs(int op);
+int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint32_t IC, uint32_t KYX, bool first,
+                       bool last);
+int ensure_wpack(bh_ctx *ctx, size_t bytes);
+
+}  // namespace bhk

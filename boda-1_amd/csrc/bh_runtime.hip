@@ -105,6 +105,7 @@ int bh_destroy(bh_ctx *c) {
   for (hipGraphExec_t g : c->graphs)
     if (g) (void)hipGraphExecDestroy(g);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->wpack) (void)hipFree(c->wpack);
   if (c->stamps) (void)hipFree(c->stamps);
   if (c->cnt) (void)hipFree(c->cnt);
   (void)hipStreamDestroy(c->stream);
@@ -235,15 +236,33 @@ int bh_sgemm_kmajor(bh_ctx *c, const float *a, const float *b, float *cc, uint32
   return bh::launch_sgemm(c, a, b, cc, M, N, K);
 }
 
-int bh_conv2d_fwd_nchw(bh_ctx *c, const float *in, const float *filts, const float *biases, float *out,
-                       uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
-                       uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
+int bh_conv2d_fwd_nchw_pk(bh_ctx *c, const float *in, const float *filts, const float *packed, const float *biases,
+                          float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+                          uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
   BH_CHECK_CTX(c);
   if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
     return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
   if (H + 2 * py < KY || W + 2 * px < KX) return bh::fail(BH_UNSUP, "conv: padded input smaller than kernel");
-  return bh::launch_conv(c, in, filts, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
+  return bh::launch_conv(c, in, filts, packed, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
+}
+
+int bh_conv2d_fwd_nchw(bh_ctx *c, const float *in, const float *filts, const float *biases, float *out,
+                       uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
+                       uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
+  return bh_conv2d_fwd_nchw_pk(c, in, filts, nullptr, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
+}
+
+size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
+  return bh::conv_filts_packed_floats(OC, IC, KY, KX);
+}
+
+int bh_conv_filts_pack(bh_ctx *c, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
+                       uint32_t KX) {
+  BH_CHECK_CTX(c);
+  if (!filts || !packed) return bh::fail(BH_ERR, "null tensor");
+  if (!OC || !IC || !KY || !KX) return bh::fail(BH_UNSUP, "conv_filts_pack: zero-sized dimension");
+  return bh::launch_conv_filts_pack(c, filts, packed, OC, IC, KY, KX);
 }
 
 int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {

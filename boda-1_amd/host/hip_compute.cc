@@ -101,7 +101,7 @@ struct hip_compute_t : public rtc_compute_t {
 
   void compile(std::vector<rtc_func_info_t> const &fis, rtc_compile_opts_t const &) override {
     for (auto const &fi : fis) {
-      bool known = fi.func_name == "hip_sgemm" || fi.func_name == "hip_conv" ||
+      bool known = fi.func_name == "hip_sgemm" || fi.func_name == "hip_conv" || fi.func_name == "hip_xpose_filts" ||
                    fi.func_name.rfind("gen_data_", 0) == 0;
       if (!known)
         unsup_err("be=hip runs the hand-written gfx950 kernels (hip_sgemm, hip_conv, gen_data_*); '" +
@@ -147,10 +147,17 @@ struct hip_compute_t : public rtc_compute_t {
       conv_shape_t s = get_conv_shape(fi.op);
       auto r = fi.op.scalars.find("conv_has_relu");
       int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
-      bh_check(bh_conv2d_fwd_nchw(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "biases", true),
-                                  arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py,
-                                  s.px, relu),
+      // filts_xp (optional): the bank hip_xpose_filts made before the timed calls
+      bh_check(bh_conv2d_fwd_nchw_pk(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
+                                     arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
+                                     s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
                "hip_conv");
+    } else if (fn == "hip_xpose_filts") {  // Boda's xpose_filts (test/rtc/xpose_filts.cucl) for hip_conv
+      conv_shape_t s = get_conv_shape(fi.op);
+      if (arg_dims(rfc, "filts_xp").elems() != bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX))
+        rt_err("hip_xpose_filts: filts_xp has the wrong size");
+      bh_check(bh_conv_filts_pack(ctx, arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp"), s.OC, s.IC, s.KY, s.KX),
+               "hip_xpose_filts");
     } else {  // gen_data_<type>_<arg>
       std::string an = fn.substr(fn.rfind('_') + 1);
       uint32_t mode = (uint32_t)arg_val(rfc, "mode", 5);

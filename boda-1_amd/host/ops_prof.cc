@@ -20,6 +20,7 @@
 #include <map>
 #include <sstream>
 
+#include "boda_hip.h"
 #include "nda_digest.H"
 #include "op_desc.H"
 #include "rtc_compute.H"
@@ -231,6 +232,20 @@ int main(int argc, char **argv) {
         rtc_func_call_t c;
         c.rtc_func_name = op.func_name;
         for (auto const &vn : arg_vars(op)) c.arg_map[vn] = vn;
+        if (op.type == "Convolution") {
+          // layout transform of the filters before the timed calls, as the reference's
+          // xpose_filts (src/rtc_prof.cc:93-99; untimed)
+          conv_shape_t s = get_conv_shape(op);
+          rtc->compile({{"hip_xpose_filts", "", {}, op}}, rtc_compile_opts_t());
+          const uint32_t nxp = (uint32_t)bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX);
+          rtc->create_var_with_dims("filts_xp", dims_t(std::vector<std::pair<std::string, uint32_t>>{{"x", nxp}}));
+          rtc_func_call_t x;
+          x.rtc_func_name = "hip_xpose_filts";
+          x.arg_map["filts"] = "filts";
+          x.arg_map["filts_xp"] = "filts_xp";
+          rtc->run(x);
+          c.arg_map["filts_xp"] = "filts_xp";
+        }
         uint32_t call_id = 0;
         for (uint32_t r = 0; r < run_iter; ++r) call_id = rtc->run(c);
         rtc->finish_and_sync();
@@ -248,6 +263,12 @@ int main(int argc, char **argv) {
           } catch (rt_exception const &) {
           }
         }
+      if (op.type == "Convolution") {
+        try {
+          rtc->release_var("filts_xp");
+        } catch (rt_exception const &) {
+        }
+      }
       rtc->release_per_call_id_data();
       rtc->release_all_funcs();
       std::string dstat = "n/a";

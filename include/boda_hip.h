@@ -139,6 +139,24 @@ int bh_conv2d_fwd_nchw(bh_ctx *ctx, const float *in, const float *filts, const f
                        uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx,
                        uint32_t py, uint32_t px, int relu);
 
+/* Filter-bank transform for the conv variants that read the filters k-major --
+ * Boda's xpose_filts (test/rtc/xpose_filts.cucl, run once per var before the
+ * timed calls: src/rtc_prof.cc:93-99, src/rtc_fwd.cc:306-326). packed receives
+ * bh_conv_filts_packed_floats(OC, IC, KY, KX) floats: row (ky*KX+kx)*IC + ic holds
+ * filts[*][ic][ky][kx] for every output channel (rows padded to a multiple of 4
+ * floats, zero rows up to a multiple of 64). */
+size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
+int bh_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC,
+                       uint32_t KY, uint32_t KX);
+/* bh_conv2d_fwd_nchw with the transformed bank of filts already made by
+ * bh_conv_filts_pack (packed may be NULL: then a variant that needs it makes it
+ * itself, inside the call). filts must still be given: variants that read the
+ * reference layout use it. */
+int bh_conv2d_fwd_nchw_pk(bh_ctx *ctx, const float *in, const float *filts, const float *packed,
+                          const float *biases, float *out, uint32_t B, uint32_t IC, uint32_t H,
+                          uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
+                          uint32_t sx, uint32_t py, uint32_t px, int relu);
+
 /* Name of the kernel variant bh_conv2d_fwd_nchw / bh_sgemm_kmajor would run
  * for a shape (op==0: sgemm with dims[0..2] = M,N,K; op==1: conv with
  * dims[0..10] = B,IC,H,W,OC,KY,KX,sy,sx,py,px). */

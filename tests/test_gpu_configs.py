@@ -24,6 +24,8 @@ CONV_SHAPES = [
     ops.ConvShape(2, 40, 8, 8, 20, 1, 1, 1, 1, 0, 0),    # 1x1, OH*OW % 4 == 0 (float4 output rows)
     ops.ConvShape(1, 8, 6, 6, 48, 3, 3, 1, 1, 1, 1),     # im2col, OH*OW % 4 == 0
     ops.ConvShape(1, 520, 4, 4, 40, 1, 1, 1, 1, 0, 0),   # 1x1, long K (register ring wraps)
+    ops.ConvShape(2, 70, 9, 7, 40, 3, 3, 1, 1, 1, 1),    # im2col, IC >= BK (ring: two-tap loader), ragged
+    ops.ConvShape(1, 64, 12, 11, 96, 5, 5, 2, 2, 2, 2),  # im2col 5x5 stride 2, IC = 64
 ]
 
 
@@ -39,6 +41,8 @@ def test_conv_config(dev, ci, splits):
             ref = orc.conv_ref(i, f, b, s, 1)
             nm, rl2, _ = orc.normalized_errors(ref, out)
             assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            # a bank transformed up front (bh_conv_filts_pack) gives the same bits
+            np.testing.assert_array_equal(run_conv(dev, s, packed=True), out)
     finally:
         dev.tune_set(1, -1, 0)
 

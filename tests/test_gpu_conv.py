@@ -25,7 +25,7 @@ NORM_TOL, RL2_TOL = 1e-4, 1e-5
 KNOWN_REF_DIGEST_OUTLIERS = {ops.ConvShape(5, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)}
 
 
-def run_conv(dev, s, mode=5, relu=1, with_bias=True, host_inputs=None):
+def run_conv(dev, s, mode=5, relu=1, with_bias=True, host_inputs=None, packed=False):
     i = dev.alloc_floats(s.B * s.IC * s.H * s.W)
     f = dev.alloc_floats(s.OC * s.K)
     b = dev.alloc_floats(s.OC)
@@ -39,9 +39,13 @@ def run_conv(dev, s, mode=5, relu=1, with_bias=True, host_inputs=None):
         i.upload(hi)
         f.upload(hf)
         b.upload(hb)
-    dev.conv(i, f, b if with_bias else None, o, s, relu)
+    pk = None
+    if packed:  # the filter-bank transform made up front (bh_conv_filts_pack), as ops-prof does
+        pk = dev.alloc_floats(boda_hip.conv_filts_packed_floats(s))
+        dev.conv_filts_pack(f, pk, s)
+    dev.conv(i, f, b if with_bias else None, o, s, relu, packed=pk)
     out = o.download()
-    for x in (i, f, b, o):
+    for x in (i, f, b, o) + ((pk,) if pk is not None else ()):
         x.free()
     return out
 

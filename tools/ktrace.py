@@ -39,6 +39,14 @@ def one(dev, wl, reps):
             v = [marks[b * 8 + k] for b in range(NSLOT // 8) if 0 < marks[b * 8 + k] <= post]
             if v:
                 pts[k] = v
+        # per-block phase durations: prologue (m1-m0), K loop (m2-m1), epilogue (m4-m2)
+        dur = {}
+        for a, b in ((0, 1), (1, 2), (2, 4)):
+            d = [marks[i * 8 + b] - marks[i * 8 + a] for i in range(NSLOT // 8)
+                 if 0 < marks[i * 8 + a] <= post and 0 < marks[i * 8 + b] <= post]
+            if d:
+                dur["%d-%d" % (a, b)] = d
+        pts["dur"] = dur
         rows.append((post, pts))
     return rows
 
@@ -47,7 +55,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--conv", action="append", default=[])
     ap.add_argument("--sgemm", action="append", default=[])
-    ap.add_argument("--cfg", type=int, default=-1)
+    ap.add_argument("--cfg", default="-1", help="config index or name")
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -56,7 +64,8 @@ def main():
     with bh.Device(0) as dev:
         for s in shapes:
             kind = 0 if isinstance(s, SgemmShape) else 1
-            dev.tune_set(kind, args.cfg, args.splits)
+            ci = int(args.cfg) if args.cfg.lstrip("-").isdigit() else bh.tune_cfg_names(kind).index(args.cfg)
+            dev.tune_set(kind, ci, args.splits)
             wl = Workload(dev, [s])
             wl.launch(0)
             dev.sync()
@@ -70,6 +79,8 @@ def main():
                         v = pts[k]
                         line += " m%d %6.2f/%6.2f/%6.2f (%d)" % (k, min(v), statistics.median(v), max(v), len(v))
                 print(line)
+                print("      per-block us (median/max): " + "  ".join(
+                    "m%s %.2f/%.2f" % (k, statistics.median(v), max(v)) for k, v in pts["dur"].items()))
             wl.free()
             dev.tune_set(kind, -1, 0)
 
