@@ -26,7 +26,9 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
-           "bh_conv_filts_packed_floats", "bh_conv_filts_pack"]
+           "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
+           "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
+           "bh_eltwise"]
 
 
 class BodaHipError(RuntimeError):
@@ -74,6 +76,14 @@ def lib():
         L.bh_conv_filts_packed_floats.argtypes = [c_u32] * 4
         L.bh_conv_filts_packed_floats.restype = ctypes.c_size_t
         L.bh_conv_filts_pack.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 4
+        L.bh_pool_out_size.argtypes = [c_u32] * 4
+        L.bh_pool_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 10 + [ctypes.c_int]
+        L.bh_lrn_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 5 + [ctypes.c_float] * 3
+        L.bh_relu_inplace.argtypes = [c_vp, c_vp, ctypes.c_uint64]
+        L.bh_softmax_chans.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 4
+        L.bh_chan_copy.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 7
+        L.bh_chan_affine.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 3 + [ctypes.c_int]
+        L.bh_eltwise.argtypes = [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
         L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
         L.bh_spin.argtypes = [c_vp, ctypes.c_int]
@@ -111,6 +121,10 @@ def variant_name(op_kind, dims):
 def conv_filts_packed_floats(s):
     """Floats of the transformed filter bank (bh_conv_filts_pack) for conv shape s."""
     return lib().bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX)
+
+
+def pool_out_size(n, k, stride, pad):
+    return lib().bh_pool_out_size(n, k, stride, pad)
 
 
 def tune_cfg_names(op_kind):
@@ -260,6 +274,31 @@ class Device:
         else:
             _check(lib().bh_conv2d_fwd_nchw_pk(self.ctx, inp.ptr, filts.ptr, packed.ptr, bp, out.ptr, s.B, s.IC, s.H,
                                                s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu)))
+
+    # ---- the other forward layers (bh_fwdops.hip)
+    def pool(self, inp, out, B, C, H, W, KY, KX, sy, sx, py, px, avg, out_in_yx=None):
+        _check(lib().bh_pool_fwd_nchw(self.ctx, inp.ptr, out.ptr, out_in_yx.ptr if out_in_yx is not None else None,
+                                      B, C, H, W, KY, KX, sy, sx, py, px, int(avg)))
+
+    def lrn(self, inp, out, B, C, H, W, local_size, alpha, beta, k, out_scale_base=None):
+        _check(lib().bh_lrn_fwd_nchw(self.ctx, inp.ptr, out.ptr,
+                                     out_scale_base.ptr if out_scale_base is not None else None,
+                                     B, C, H, W, local_size, alpha, beta, k))
+
+    def relu(self, x, n):
+        _check(lib().bh_relu_inplace(self.ctx, x.ptr, n))
+
+    def softmax(self, inp, prob, B, C, H, W):
+        _check(lib().bh_softmax_chans(self.ctx, inp.ptr, prob.ptr, B, C, H, W))
+
+    def chan_copy(self, inp, out, B, HW, in_c, ic0, out_c, oc0, nc):
+        _check(lib().bh_chan_copy(self.ctx, inp.ptr, out.ptr, B, HW, in_c, ic0, out_c, oc0, nc))
+
+    def chan_affine(self, inp, out, scale, shift, B, C, HW, relu=0):
+        _check(lib().bh_chan_affine(self.ctx, inp.ptr, out.ptr, scale.ptr, shift.ptr, B, C, HW, int(relu)))
+
+    def eltwise(self, a, b, out, n, op=1, relu=0):
+        _check(lib().bh_eltwise(self.ctx, a.ptr, b.ptr, out.ptr, n, op, int(relu)))
 
     def conv_filts_pack(self, filts, packed, s):
         """Boda's xpose_filts counterpart: write the k-major bank of filts into packed."""

@@ -82,6 +82,18 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX);
+uint32_t pool_out_sz(uint32_t in, uint32_t k, uint32_t s, uint32_t p);
+int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C, uint32_t H,
+                uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int avg);
+int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
+               uint32_t W, uint32_t local_size, float alpha, float beta, float k);
+int launch_relu(bh_ctx *ctx, float *x, uint64_t n);
+int launch_softmax(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W);
+int launch_chan_copy(bh_ctx *ctx, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
+                     uint32_t out_c, uint32_t oc0, uint32_t nc);
+int launch_chan_affine(bh_ctx *ctx, const float *in, float *out, const float *scale, const float *shift, uint32_t B,
+                       uint32_t C, uint32_t HW, int relu);
+int launch_eltwise(bh_ctx *ctx, const float *a, const float *b, float *out, uint64_t n, int op, int relu);
 std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
 std::string conv_variant(const uint32_t *d);
 int tune_set(bh_ctx *ctx, int op, int cfg, int splits);

@@ -1,0 +1,267 @@
+// bh_fwdops.hip -- the non-conv forward layers of Boda's net executor (conv_pipe_fwd_t,
+// src/rtc_fwd.cc:263-405) as gfx950 kernels: Pooling, LRN, ReLU, Softmax, and the channel
+// copies behind Concat / Split. All are HBM-bound (a few flops per byte): one pass over the
+// input, coalesced along x (or along the flat index), results as the reference kernels
+// compute them (test/rtc/{pool,lrn,relu,softmax,copy,split_copy}.cucl).
+#include "bh_common.h"
+
+#include <cfloat>
+
+namespace {
+
+// Pooling (test/rtc/pool.cucl): one thread per output element; only non-padding pixels
+// count, for max and for average (the average divides by the number of in-image taps).
+// out_in_yx (may be null): for max pooling, the in_y*W + in_x of the winning input (-1 if
+// none), stored as a float as the reference does.
+__global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                   float *__restrict__ out_in_yx, uint32_t total, uint32_t C,
+                                                   uint32_t H, uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY,
+                                                   uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
+                                                   int avg) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t ox = i % OW, t = i / OW, oy = t % OH, nc = t / OH;  // nc = img * C + chan
+  const float *const src = in + (size_t)nc * H * W;
+  float v = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
+  int oyx = -1;
+  // the reference's loop order (kx outer, ky inner) decides ties and the summation order
+  for (uint32_t kx = 0; kx < KX; ++kx)
+    for (uint32_t ky = 0; ky < KY; ++ky) {
+      const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
+      if (iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H) {
+        const float x = src[iy * W + ix];
+        if (avg) {
+          v += x;
+          cnt += 1.0f;
+        } else if (x > v) {
+          v = x;
+          oyx = iy * (int)W + ix;
+        }
+      }
+    }
+  if (avg) v /= cnt;
+  out[i] = v;
+  if (out_in_yx) out_in_yx[i] = (float)oyx;
+  (void)C;
+}
+
+// LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): one thread per (img, y, x), a
+// running sum of squares over a window of LS channels kept with a ring of the last LS inputs
+// (+ new^2 - old^2, the reference's order), out = in * (k + alpha/LS * sum)^-beta.
+template <int LS>
+__global__ __launch_bounds__(256) void lrn_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                  float *__restrict__ out_scale_base, uint32_t npix, uint32_t C,
+                                                  uint32_t HW, float alpha, float beta, float k) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix) return;
+  const uint32_t img = i / HW, pix = i - img * HW;
+  const size_t base = (size_t)img * C * HW + pix;
+  constexpr int hls = LS >> 1;
+  const float alpha_over_ls = alpha / (float)LS;
+  float ring[LS];
+#pragma unroll
+  for (int j = 0; j < LS; ++j) ring[j] = 0.0f;
+  float sum = 0.0f;
+  const int n = (int)C + hls;
+  for (int c0 = 0; c0 < n; c0 += LS) {
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {  // channel c = c0 + j sits in ring slot j (c % LS)
+      const int c = c0 + j;
+      if (c < n) {
+        const float old = ring[j];
+        ring[j] = c < (int)C ? in[base + (size_t)c * HW] : 0.0f;
+        sum += ring[j] * ring[j];
+        sum -= old * old;
+        if (c >= hls) {
+          const int oc = c - hls;
+          const float sb = k + sum * alpha_over_ls;
+          if (out_scale_base) out_scale_base[base + (size_t)oc * HW] = sb;
+          out[base + (size_t)oc * HW] = ring[(j + LS - hls) % LS] * powf(sb, -beta);
+        }
+      }
+    }
+  }
+}
+
+// ReLU in place (test/rtc/relu.cucl): x <= 0 -> 0.
+__global__ __launch_bounds__(256) void relu_kernel(float *__restrict__ x, uint64_t n) {
+  const uint64_t n4 = n / 4;
+  float4 *const x4 = (float4 *)x;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256) {
+    float4 v = x4[i];
+    v.x = v.x <= 0.0f ? 0.0f : v.x;
+    v.y = v.y <= 0.0f ? 0.0f : v.y;
+    v.z = v.z <= 0.0f ? 0.0f : v.z;
+    v.w = v.w <= 0.0f ? 0.0f : v.w;
+    x4[i] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n4 * 4) {
+    float &v = x[n4 * 4 + threadIdx.x];
+    v = v <= 0.0f ? 0.0f : v;
+  }
+}
+
+// Softmax over channels per pixel (test/rtc/softmax.cucl): max starts at 0 (as the reference),
+// exp(x - max), then divide by the sum.
+__global__ __launch_bounds__(256) void softmax_kernel(const float *__restrict__ in, float *__restrict__ prob,
+                                                      uint32_t npix, uint32_t C, uint32_t HW) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix) return;
+  const uint32_t img = i / HW, pix = i - img * HW;
+  const size_t base = (size_t)img * C * HW + pix;
+  float mx = 0.0f, sum = 0.0f;
+  for (uint32_t c = 0; c < C; ++c) mx = fmaxf(mx, in[base + (size_t)c * HW]);
+  for (uint32_t c = 0; c < C; ++c) {
+    const float v = expf(in[base + (size_t)c * HW] - mx);
+    prob[base + (size_t)c * HW] = v;
+    sum += v;
+  }
+  for (uint32_t c = 0; c < C; ++c) prob[base + (size_t)c * HW] /= sum;
+}
+
+// Channel-slab copy between NCHW tensors of equal H x W: out[img][c + oc0] = in[img][c + ic0]
+// for c < nc (Concat: copy.cucl with ocix; Split: split_copy.cucl with icix). Each image's
+// slab is contiguous on both sides: float4 when both offsets are 16-B aligned.
+__global__ __launch_bounds__(256) void chan_copy_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                        uint32_t B, uint64_t slab, uint64_t in_img, uint64_t out_img,
+                                                        uint64_t in_off, uint64_t out_off, int vec) {
+  const uint32_t img = blockIdx.y;
+  const float *const s = in + img * in_img + in_off;
+  float *const d = out + img * out_img + out_off;
+  if (vec) {
+    const uint64_t n4 = slab / 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256)
+      ((float4 *)d)[i] = ((const float4 *)s)[i];
+  } else {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < slab; i += (uint64_t)gridDim.x * 256) d[i] = s[i];
+  }
+  (void)B;
+}
+
+// Per-channel affine y = x * scale[c] + shift[c] (+ ReLU): inference BatchNorm followed by
+// Scale, folded (resnet prototxts; not in the reference's rtc_fwd). One block row
+// per (img, chan) slab, float4 along the pixels when HW % 4 == 0.
+__global__ __launch_bounds__(256) void chan_affine_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          const float *__restrict__ scale,
+                                                          const float *__restrict__ shift, uint32_t C, uint32_t HW,
+                                                          int relu) {
+  const uint32_t nc = blockIdx.y, c = nc % C;
+  const float a = scale[c], b = shift[c];
+  const size_t base = (size_t)nc * HW;
+  if (HW % 4 == 0) {
+    const float4 *s = (const float4 *)(in + base);
+    float4 *d = (float4 *)(out + base);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < HW / 4; i += gridDim.x * 256) {
+      float4 v = s[i];
+      v.x = fmaf(v.x, a, b); v.y = fmaf(v.y, a, b); v.z = fmaf(v.z, a, b); v.w = fmaf(v.w, a, b);
+      if (relu) {
+        v.x = v.x <= 0.0f ? 0.0f : v.x; v.y = v.y <= 0.0f ? 0.0f : v.y;
+        v.z = v.z <= 0.0f ? 0.0f : v.z; v.w = v.w <= 0.0f ? 0.0f : v.w;
+      }
+      d[i] = v;
+    }
+  } else {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < HW; i += gridDim.x * 256) {
+      float v = fmaf(in[base + i], a, b);
+      out[base + i] = (relu && v <= 0.0f) ? 0.0f : v;
+    }
+  }
+}
+
+// Elementwise combine of two tensors (Caffe Eltwise: 0 PROD, 1 SUM, 2 MAX) (+ ReLU).
+__global__ __launch_bounds__(256) void eltwise_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                      float *__restrict__ out, uint64_t n, int op, int relu) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const float x = a[i], y = b[i];
+    float v = op == 0 ? x * y : (op == 1 ? x + y : fmaxf(x, y));
+    out[i] = (relu && v <= 0.0f) ? 0.0f : v;
+  }
+}
+
+uint32_t grid_for(uint64_t n, uint32_t cap = 16384) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap));
+}
+
+}  // namespace
+
+namespace bh {
+
+uint32_t pool_out_sz(uint32_t in, uint32_t k, uint32_t s, uint32_t p) {
+  // Caffe pooling: a partial last window makes one more output (src/conv_util.cc:198-204)
+  const uint32_t pin = in + 2 * p;
+  if (pin < k) return 1;
+  return (pin - k + s - 1) / s + 1;
+}
+
+int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C, uint32_t H,
+                uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int avg) {
+  const uint32_t OH = pool_out_sz(H, KY, sy, py), OW = pool_out_sz(W, KX, sx, px);
+  const uint64_t total = (uint64_t)B * C * OH * OW;
+  if (total >= (1ull << 31) || (uint64_t)B * C * H * W >= (1ull << 31)) return fail(BH_UNSUP, "pool: tensor too large");
+  uint32_t tot = (uint32_t)total;
+  void *args[] = {&in, &out, &out_in_yx, &tot, &C, &H, &W, (void *)&OH, (void *)&OW, &KY, &KX, &sy, &sx, &py, &px, &avg};
+  return launch(ctx, (const void *)pool_kernel, dim3((tot + 255) / 256), dim3(256), args, true, true, "pool");
+}
+
+int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
+               uint32_t W, uint32_t local_size, float alpha, float beta, float k) {
+  const uint64_t np = (uint64_t)B * H * W;
+  if (np * C >= (1ull << 31)) return fail(BH_UNSUP, "lrn: tensor too large");
+  uint32_t npix = (uint32_t)np, HW = H * W;
+  void *args[] = {&in, &out, &out_scale_base, &npix, &C, &HW, &alpha, &beta, &k};
+  const void *kern = nullptr;
+  switch (local_size) {
+    case 1: kern = (const void *)lrn_kernel<1>; break;
+    case 3: kern = (const void *)lrn_kernel<3>; break;
+    case 5: kern = (const void *)lrn_kernel<5>; break;
+    case 7: kern = (const void *)lrn_kernel<7>; break;
+    case 9: kern = (const void *)lrn_kernel<9>; break;
+    case 11: kern = (const void *)lrn_kernel<11>; break;
+    default: return fail(BH_UNSUP, "lrn: local_size must be odd and <= 11");
+  }
+  return launch(ctx, kern, dim3((npix + 255) / 256), dim3(256), args, true, true, "lrn");
+}
+
+int launch_relu(bh_ctx *ctx, float *x, uint64_t n) {
+  if ((uintptr_t)x % 16) return fail(BH_UNSUP, "relu: pointer must be 16-byte aligned");
+  void *args[] = {&x, &n};
+  return launch(ctx, (const void *)relu_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), args, true, true, "relu");
+}
+
+int launch_softmax(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W) {
+  const uint64_t np = (uint64_t)B * H * W;
+  if (np * C >= (1ull << 31)) return fail(BH_UNSUP, "softmax: tensor too large");
+  uint32_t npix = (uint32_t)np, HW = H * W;
+  void *args[] = {&in, &prob, &npix, &C, &HW};
+  return launch(ctx, (const void *)softmax_kernel, dim3((npix + 255) / 256), dim3(256), args, true, true, "softmax");
+}
+
+int launch_chan_copy(bh_ctx *ctx, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
+                     uint32_t out_c, uint32_t oc0, uint32_t nc) {
+  if (ic0 + nc > in_c || oc0 + nc > out_c) return fail(BH_ERR, "chan_copy: channel range out of bounds");
+  uint64_t slab = (uint64_t)nc * HW, in_img = (uint64_t)in_c * HW, out_img = (uint64_t)out_c * HW;
+  uint64_t in_off = (uint64_t)ic0 * HW, out_off = (uint64_t)oc0 * HW;
+  int vec = (slab % 4 == 0 && in_img % 4 == 0 && out_img % 4 == 0 && in_off % 4 == 0 && out_off % 4 == 0 &&
+             (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0);
+  if (!B || !slab) return BH_OK;
+  void *args[] = {&in, &out, &B, &slab, &in_img, &out_img, &in_off, &out_off, &vec};
+  uint32_t gx = grid_for(vec ? slab / 4 : slab, 4096);
+  return launch(ctx, (const void *)chan_copy_kernel, dim3(gx, B), dim3(256), args, true, true, "chan_copy");
+}
+
+int launch_chan_affine(bh_ctx *ctx, const float *in, float *out, const float *scale, const float *shift, uint32_t B,
+                       uint32_t C, uint32_t HW, int relu) {
+  if ((uint64_t)B * C > 65535u * 1024u || !B || !C || !HW) return fail(BH_UNSUP, "chan_affine: bad extent");
+  if (HW % 4 == 0 && ((uintptr_t)in % 16 || (uintptr_t)out % 16)) return fail(BH_UNSUP, "chan_affine: unaligned");
+  uint32_t gx = grid_for(HW % 4 == 0 ? HW / 4 : HW, 64);
+  void *args[] = {&in, &out, &scale, &shift, &C, &HW, &relu};
+  return launch(ctx, (const void *)chan_affine_kernel, dim3(gx, B * C), dim3(256), args, true, true, "chan_affine");
+}
+
+int launch_eltwise(bh_ctx *ctx, const float *a, const float *b, float *out, uint64_t n, int op, int relu) {
+  if (op < 0 || op > 2) return fail(BH_UNSUP, "eltwise: op must be 0 (PROD), 1 (SUM) or 2 (MAX)");
+  void *args[] = {&a, &b, &out, &n, &op, &relu};
+  return launch(ctx, (const void *)eltwise_kernel, dim3(grid_for(n)), dim3(256), args, true, true, "eltwise");
+}
+
+}  // namespace bh

@@ -253,6 +253,64 @@ int bh_conv2d_fwd_nchw(bh_ctx *c, const float *in, const float *filts, const flo
   return bh_conv2d_fwd_nchw_pk(c, in, filts, nullptr, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
 }
 
+int bh_pool_out_size(uint32_t in, uint32_t k, uint32_t stride, uint32_t pad) {
+  if (!k || !stride) return 0;
+  return (int)bh::pool_out_sz(in, k, stride, pad);
+}
+
+int bh_pool_fwd_nchw(bh_ctx *c, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C, uint32_t H,
+                     uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
+                     int avg) {
+  BH_CHECK_CTX(c);
+  if (!in || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !C || !H || !W || !KY || !KX || !sy || !sx) return bh::fail(BH_UNSUP, "pool: zero-sized dimension");
+  if (py >= KY || px >= KX) return bh::fail(BH_UNSUP, "pool: padding must be smaller than the window");
+  return bh::launch_pool(c, in, out, out_in_yx, B, C, H, W, KY, KX, sy, sx, py, px, avg ? 1 : 0);
+}
+
+int bh_lrn_fwd_nchw(bh_ctx *c, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
+                    uint32_t W, uint32_t local_size, float alpha, float beta, float k) {
+  BH_CHECK_CTX(c);
+  if (!in || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !C || !H || !W) return bh::fail(BH_UNSUP, "lrn: zero-sized dimension");
+  return bh::launch_lrn(c, in, out, out_scale_base, B, C, H, W, local_size, alpha, beta, k);
+}
+
+int bh_relu_inplace(bh_ctx *c, float *x, uint64_t n) {
+  BH_CHECK_CTX(c);
+  if (!x) return bh::fail(BH_ERR, "null tensor");
+  if (!n) return BH_OK;
+  return bh::launch_relu(c, x, n);
+}
+
+int bh_softmax_chans(bh_ctx *c, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W) {
+  BH_CHECK_CTX(c);
+  if (!in || !prob) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !C || !H || !W) return bh::fail(BH_UNSUP, "softmax: zero-sized dimension");
+  return bh::launch_softmax(c, in, prob, B, C, H, W);
+}
+
+int bh_chan_copy(bh_ctx *c, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
+                 uint32_t out_c, uint32_t oc0, uint32_t nc) {
+  BH_CHECK_CTX(c);
+  if (!in || !out) return bh::fail(BH_ERR, "null tensor");
+  return bh::launch_chan_copy(c, in, out, B, HW, in_c, ic0, out_c, oc0, nc);
+}
+
+int bh_chan_affine(bh_ctx *c, const float *in, float *out, const float *scale, const float *shift, uint32_t B,
+                   uint32_t C, uint32_t HW, int relu) {
+  BH_CHECK_CTX(c);
+  if (!in || !out || !scale || !shift) return bh::fail(BH_ERR, "null tensor");
+  return bh::launch_chan_affine(c, in, out, scale, shift, B, C, HW, relu ? 1 : 0);
+}
+
+int bh_eltwise(bh_ctx *c, const float *a, const float *b, float *out, uint64_t n, int op, int relu) {
+  BH_CHECK_CTX(c);
+  if (!a || !b || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!n) return BH_OK;
+  return bh::launch_eltwise(c, a, b, out, n, op, relu ? 1 : 0);
+}
+
 size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
   return bh::conv_filts_packed_floats(OC, IC, KY, KX);
 }

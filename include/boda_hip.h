@@ -157,6 +157,40 @@ int bh_conv2d_fwd_nchw_pk(bh_ctx *ctx, const float *in, const float *filts, cons
                           uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
                           uint32_t sx, uint32_t py, uint32_t px, int relu);
 
+/* ---- the other forward layers of Boda's net executor (conv_pipe_fwd_t::gen_op,
+ *      src/rtc_fwd.cc:263-405), NCHW fp32 ------------------------------------ */
+/* Pooling (test/rtc/pool.cucl; Caffe output size, a partial last window adds an
+ * output: src/conv_util.cc:198-204): max (avg=0) or average (avg=1) over the
+ * in-image taps of each KY x KX window. out_in_yx (may be NULL): max pooling's
+ * winning in_y*W+in_x per output, as float (-1: none). Global pooling: KY=H,
+ * KX=W, strides 1, no padding. */
+int bh_pool_out_size(uint32_t in, uint32_t k, uint32_t stride, uint32_t pad);
+int bh_pool_fwd_nchw(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C,
+                     uint32_t H, uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py,
+                     uint32_t px, int avg);
+/* LRN across channels (test/rtc/lrn.cucl, Caffe-matching running sum):
+ * out = in * (k + alpha/local_size * sum of squares over local_size channels)^-beta;
+ * out_scale_base (may be NULL) receives the base. local_size odd, <= 11. */
+int bh_lrn_fwd_nchw(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C,
+                    uint32_t H, uint32_t W, uint32_t local_size, float alpha, float beta, float k);
+/* ReLU in place (test/rtc/relu.cucl); x 16-byte aligned, n elements. */
+int bh_relu_inplace(bh_ctx *ctx, float *x, uint64_t n);
+/* Softmax over channels per pixel (test/rtc/softmax.cucl). */
+int bh_softmax_chans(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W);
+/* Channel-slab copy between NCHW tensors of equal H*W = HW: out[img][oc0 + c] =
+ * in[img][ic0 + c] for c < nc. Concat (test/rtc/copy.cucl, ocix) and Split
+ * (test/rtc/split_copy.cucl, icix). */
+int bh_chan_copy(bh_ctx *ctx, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
+                 uint32_t out_c, uint32_t oc0, uint32_t nc);
+
+/* Beyond the reference's rtc_fwd (it rejects these), for resnet nets:
+ * per-channel affine out = in * scale[c] + shift[c] (+ReLU) -- inference BatchNorm
+ * and Scale folded -- over B x C x HW; and Caffe Eltwise of two equal-size tensors,
+ * op 0 PROD, 1 SUM, 2 MAX (+ReLU). */
+int bh_chan_affine(bh_ctx *ctx, const float *in, float *out, const float *scale, const float *shift, uint32_t B,
+                   uint32_t C, uint32_t HW, int relu);
+int bh_eltwise(bh_ctx *ctx, const float *a, const float *b, float *out, uint64_t n, int op, int relu);
+
 /* Name of the kernel variant bh_conv2d_fwd_nchw / bh_sgemm_kmajor would run
  * for a shape (op==0: sgemm with dims[0..2] = M,N,K; op==1: conv with
  * dims[0..10] = B,IC,H,W,OC,KY,KX,sy,sx,py,px). */

@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--timing", choices=["graph", "flush"], default="graph")
     ap.add_argument("--max-flop-sgemm", type=float, default=3e12, help="skip sgemm sweeps above this (use heuristic)")
+    ap.add_argument("--merge", action="store_true", help="keep --out entries of ops not swept in this run")
     args = ap.parse_args()
     global TIMING
     TIMING = args.timing
@@ -148,11 +149,21 @@ def main():
                 key, t_def, names[kind][best[1]] if best[1] >= 0 else "default", best[2], best[0], rf,
                 100 * rf / best[0]), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    lines = {k: "%s cfg=%s splits=%d red=%s" % (k, cn, abs(S), "k" if S < 0 else "i")
+             for k, (cn, S, t, td) in table.items()}
+    if args.merge and os.path.exists(args.out):
+        old = {}
+        for l in open(args.out):
+            if l.startswith("#") or " cfg=" not in l:
+                continue
+            old[l[:l.index(" cfg=")]] = l.rstrip("\n")
+        old.update(lines)
+        lines = old
     with open(args.out, "w") as f:
         f.write("# boda-1_amd tuning table (tools/tune.py) for %s; <op> <dims> cfg=<tile config> splits=<K splits>\n"
                 % plat)
-        for k, (cn, S, t, td) in table.items():
-            f.write("%s cfg=%s splits=%d red=%s\n" % (k, cn, abs(S), "k" if S < 0 else "i"))
+        for k in sorted(lines, key=lambda k: (k.split()[0], [int(x) for x in k.split()[1:]])):
+            f.write(lines[k] + "\n")
     if args.json:
         json.dump({"plat": plat, "results": results}, open(args.json, "w"))
     print("wrote %d entries to %s in %.0f s" % (len(table), args.out, time.time() - t_start))
