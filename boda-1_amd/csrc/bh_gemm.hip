@@ -751,6 +751,8 @@ cfg_t sgemm_cfg(const char *name) {
 // Tile configurations (BM x BN x BK; 32x32 MFMA tiles per wave TM x TN; waves M x N).
 std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
   for (auto const &c : ring_cfgs(op)) v.push_back(c);
+  if (op == 1)
+    for (auto const &c : gv_cfgs()) v.push_back(c);
   return v;
 }
 
@@ -905,7 +907,8 @@ choice_t heuristic(int op, const uint32_t *d) {
   // split-K combined by the reduce kernel (the tuning table refines both)
   const char *n = "128x128x32";
   uint64_t tiles128 = ((OC + 127) / 128) * ((N + 127) / 128);
-  if (N <= 32) n = "128x32x32";
+  if (N <= 64 && (uint64_t)OC * K >= (1u << 20) && K % 4 == 0) n = N <= 16 ? "gv64x16" : (N <= 32 ? "gv64x32" : "gv32x64");
+  else if (N <= 32) n = "128x32x32";
   else if (OC <= 32) n = "32x256x32";
   else if (OC <= 64) n = "64x128x32";
   else if (tiles128 < 256 && K >= 256) n = "128x32x32";
@@ -948,6 +951,54 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   const uint64_t nblk = (uint64_t)p.tiles_m * p.tiles_n;
   if (nblk > 0x7fffffffu) return bh::fail(BH_UNSUP, std::string(what) + ": grid too large");
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  p.tbm = c.BM;
+  p.tbn = c.BN;
+  if (c.gv) {
+    // filter-streaming kernel (bh_gv.hip): one block per (64-row tile, K chunk); the K chunks
+    // of a tile are combined by its last arriver. ch.splits = K chunks (0: ~1024 blocks)
+    kern_t k = c.k[ald][bld][0];
+    if (!k) return bh::fail(BH_ERR, std::string(what) + ": gv loader not instantiated");
+    const uint32_t gran = (uint32_t)c.BK;  // K chunks: multiples of 16 per wave
+    const uint32_t ktg = (p.K + gran - 1) / gran;
+    uint32_t S = ch.splits ? ch.splits : (uint32_t)std::max<uint64_t>(1, (1024 + nblk - 1) / nblk);
+    S = std::max(1u, std::min(S, ktg));
+    p.ks = ((ktg + S - 1) / S) * gran;
+    S = (p.K + p.ks - 1) / p.ks;
+    void *args[] = {&p};
+    if (S > 1) {
+      int rc = ensure_ws(ctx, (size_t)S * nblk * c.BM * c.BN * 4);
+      if (rc == BH_OK) rc = ensure_cnt(ctx, nblk);
+      if (rc != BH_OK) return rc;
+      p.ws = (float *)ctx->ws;
+      p.cnt = (uint32_t *)ctx->cnt;
+    }
+    return bh::launch(ctx, (const void *)k, dim3((uint32_t)nblk, S, 1), dim3(c.NT), args, first, true, what);
+  }
+  if (c.streamk) {
+    // persistent stream-K grid (srk_kernel): ncu x blocks-per-CU blocks share the op's
+    // (tile, K tile) iterations equally; ch.splits overrides blocks per CU
+    kern_t k = c.k[ald][bld][0];
+    if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
+    const uint32_t ipt = (p.K + c.BK - 1) / c.BK;
+    const uint64_t total = nblk * ipt;
+    if (total >= (1ull << 31)) return bh::fail(BH_UNSUP, std::string(what) + ": too many K iterations");
+    uint32_t bpc = ch.splits ? std::min<uint32_t>(ch.splits, 4) : std::max(1, std::min(2, 163840 / c.lds_bytes));
+    uint64_t G = (uint64_t)ncu * bpc;
+    const uint32_t ipb = (uint32_t)((total + G - 1) / G);
+    G = (total + ipb - 1) / ipb;
+    p.ipt = ipt;
+    p.ipb = ipb;
+    p.total_it = (uint32_t)total;
+    set_fd(ipt, p.ipt_m, p.ipt_s);
+    set_fd(p.tiles_m, p.tm_m, p.tm_s);
+    int rc = ensure_ws(ctx, (size_t)2 * G * c.BM * c.BN * 4);
+    if (rc == BH_OK) rc = ensure_cnt(ctx, nblk);
+    if (rc != BH_OK) return rc;
+    p.ws = (float *)ctx->ws;
+    p.cnt = (uint32_t *)ctx->cnt;
+    void *args[] = {&p};
+    return bh::launch(ctx, (const void *)k, dim3((uint32_t)G, 1, 1), dim3(c.NT), args, first, true, what);
+  }
   const uint32_t S = resolve_splits(c, ch, p.M, p.N, p.K, ncu);
   const uint32_t nkt = (p.K + c.BK - 1) / c.BK;
   p.ks = ((nkt + S - 1) / S) * c.BK;
@@ -959,8 +1010,6 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   kern_t k = c.k[ald][bld][red];
   if (!k) return bh::fail(BH_ERR, std::string(what) + ": loader combination not instantiated");
   void *args[] = {&p};
-  p.tbm = c.BM;
-  p.tbn = c.BN;
   if (S > 1) {
     int rc = ensure_ws(ctx, (size_t)S * nblk * c.BM * c.BN * 4);
     if (rc != BH_OK) return rc;
@@ -1004,6 +1053,8 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
     bool k1 = d[5] == 1 && d[6] == 1 && d[7] == 1 && d[8] == 1 && d[9] == 0 && d[10] == 0;
     s = std::string("mfma32_conv_") + (k1 ? "1x1_" : "im2col_") + c.name + ((K % 4 == 0) ? "_avec" : "_ascalar");
   }
+  if (c.streamk) return s + "_streamk";
+  if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
   uint32_t S = resolve_splits(c, ch, M, N, K, 256);
   if (S > 1) {
     uint64_t nblk = (uint64_t)((M + c.BM - 1) / c.BM) * ((N + c.BN - 1) / c.BN);
@@ -1091,6 +1142,16 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   const bool avec = (K % 4 == 0) && ((uintptr_t)filts % 16 == 0);
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
+  if (cfgs(1)[ch.cfg].gv) {
+    // few output columns: stream the bank in its reference layout; the window covering the
+    // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
+    const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
+    if (avec)
+      return launch_gemm(ctx, 1, ch, A_MVEC, fc ? B_FC : (k1 ? B_IM1X1 : B_IM2COL), p, "conv");
+    ch = choice_t{};  // unaligned bank (K % 4 or pointer): a tile kernel
+    ch.cfg = cfg_index(1, "128x32x32");
+    ch.red = 1;
+  }
   if (cfgs(1)[ch.cfg].packA) {
     // ring kernels read the filter bank k-major: repack it first (this call's first dispatch)
     // (K order (ky, kx, ic), rows padded to a multiple of 64; input offsets + 2^30 must miss)

@@ -11,7 +11,9 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
-enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5 };
+enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, NBLD = 7 };
+// B_FC: the im2col of a conv whose window covers the whole (unpadded) input -- Boda's ipconv /
+// InnerProduct-as-conv -- is the input itself: column n = image n, X[k][n] = in[n * K + k]
 // B_IMT2: ring kernels' im2col when IC >= BK: a wave's rows of one K tile touch at most two
 // filter taps (ring kernels read K in (ky, kx, ic) order)
 // B_IM1X1V: 1x1 conv whose OH*OW % 4 == 0 with a 16-B aligned input: four adjacent output
@@ -39,6 +41,8 @@ struct GemmArgs {
   uint32_t H, W, KX, KYX, sy, sx, py, px, OW, OHW, HW, ICHW, OCOHW;
   uint32_t kyx_m, kyx_s, kx_m, kx_s, ohw_m, ohw_s, ow_m, ow_s;  // fastdiv constants
   uint32_t IC, ic_m, ic_s;  // ring kernels: K order (ky, kx, ic) of the repacked filter bank
+  // stream-K kernels (srk_kernel): K tiles per output tile, per block, in total; fastdiv of ipt
+  uint32_t ipt, ipb, total_it, ipt_m, ipt_s, tm_m, tm_s;  // + fastdiv of tiles_m
 #ifdef BH_KTRACE
   unsigned long long *trace;  // per-block device-clock marks (tools/ktrace.py)
 #endif
@@ -230,13 +234,18 @@ typedef void (*kern_t)(GemmArgs);
 struct cfg_t {
   const char *name;
   int BM, BN, BK, NT;
-  kern_t k[4][6][3];  // [A loader][B loader][SPL]
+  kern_t k[4][NBLD][3];  // [A loader][B loader][SPL]
   int packA;          // conv: A is the filter bank repacked k-major [K][OC4] (bh_ring.hip)
+  int streamk = 0;    // persistent stream-K grid (srk_kernel): k[..][..][0] only
+  int lds_bytes = 0;  // static LDS per block (stream-K grid sizing)
+  int gv = 0;         // filter-streaming kernel (bh_gv.hip): grid (M / BM) x K chunks, BN >= N
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and
 // the repack itself (into the context's wpack buffer; first dispatch of a conv call)
 std::vector<cfg_t> ring_cfgs(int op);
+// bh_gv.hip: filter-streaming configurations for convs with few output columns
+std::vector<cfg_t> gv_cfgs();
 int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint32_t IC, uint32_t KYX, bool first,
                        bool last);
 int ensure_wpack(bh_ctx *ctx, size_t bytes);

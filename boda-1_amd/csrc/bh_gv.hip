@@ -1,0 +1,236 @@
+// bh_gv.hip -- filter-streaming kernel for convolutions with few output columns.
+//
+// Boda's ipconv variant (src/cnn_op.cc:46-68, test/rtc/ipconv.cucl) and the fully connected
+// layers run as convolutions whose output is a handful of columns: N = B*OH*OW is 1..64 while
+// the filter bank is up to 151 MB (fc6: 4096 x 256*6*6). Such an op is a matrix-vector
+// product bounded by streaming the filter bank from HBM once (53 of the 204
+// conv ops are HBM-bound). The tile kernels read the bank through a 128-row LDS tile and an
+// MFMA tile mostly wasted on padding columns; here
+//  * the bank is read in its reference layout (OC x IC*KY*KX, row-major) straight into
+//    registers with 16-B buffer loads -- each filter element is used by exactly one wave, so
+//    there is nothing to share through LDS -- and a wave keeps its whole 64-deep K batch of
+//    loads (R row tiles x 4 x 16 B per lane) in flight before the MFMAs consume them;
+//  * v_mfma_f32_16x16x4_f32 (exact fp32; 16 output columns per tile, C tiles cover N): lane
+//    (i = l & 15, g = l >> 4) holds rows/columns i and k = 4g + q of MFMA step q, so a lane's
+//    16-B load of 4 consecutive k feeds four MFMA steps (a valid reduction order: A and B
+//    use the same k map);
+//  * the four waves of a block split the block's K chunk; their partial tiles are summed
+//    through LDS in wave order, and the K chunks of a row tile (grid.y) are combined by the
+//    tile's last-arriving block in chunk order (the split-K protocol of bh_gemm.hip) -- the
+//    result is bitwise reproducible.
+// Column operand loaders: B_FC (the input itself, 16-B loads along k), B_IM1X1 and B_IM2COL
+// (scalar gathers by the implicit-im2col formulas of the tile kernels).
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+namespace {
+
+typedef float f32x4t __attribute__((ext_vector_type(4)));
+
+// NW waves split the block's K chunk; NG 16-deep k groups per register batch; DB: the next
+// batch's loads are issued before this batch's MFMAs (register double buffer)
+template <int R, int C, int NW, int NG, int DB, int BLD>
+__global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
+  constexpr int NT = NW * 64, BMr = 16 * R, NC = 16 * C, KB = 16 * NG;
+  constexpr int TSZ = BMr * NC;         // floats of a block's output tile
+  constexpr int NCH = TSZ / 4, CH = (NCH + NT - 1) / NT;
+  static_assert(NCH % NT == 0 || NT % NCH == 0, "float4 chunks per thread");
+  __shared__ __attribute__((aligned(16))) float red[NW * TSZ + 4];
+  uint32_t *const flag = (uint32_t *)(red + NW * TSZ);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m, split = blockIdx.y;
+  const uint32_t tile = blockIdx.x;
+  const uint32_t m0 = tm * BMr;
+  // this wave's share of the block's K chunk (p.ks: a multiple of NW * 16)
+  const uint32_t kq = p.ks / NW;
+  const uint32_t kw0 = split * p.ks + wave * kq;
+  const uint32_t kw1 = min(p.K, kw0 + kq);
+  const int i = lane & 15, g = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
+  // per-lane row offsets of the R row tiles (OOB past M)
+  uint32_t arow[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t m = m0 + 16 * r + i;
+    arow[r] = oob_unless(m < p.M, m * p.lda * 4u);
+  }
+  // per-lane column state of the C column tiles
+  uint32_t bcol[C];
+  int iy0[C], ix0[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const uint32_t n = tn * NC + 16 * c + i;
+    iy0[c] = 0;
+    ix0[c] = 0;
+    if constexpr (BLD == B_FC) {
+      bcol[c] = oob_unless(n < p.N, n * p.K * 4u);
+    } else {
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+      if constexpr (BLD == B_IM1X1) {
+        bcol[c] = oob_unless(n < p.N, (img * p.ICHW + pix) * 4u);
+      } else {
+        const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
+        iy0[c] = (int)(oy * p.sy) - (int)p.py;
+        ix0[c] = (int)(ox * p.sx) - (int)p.px;
+        bcol[c] = (uint32_t)((int)(img * p.ICHW) + iy0[c] * (int)p.W + ix0[c]);
+        if (n >= p.N) iy0[c] = -(1 << 29);  // every tap misses
+      }
+    }
+  }
+  // column operand of tile c, k = k4 .. k4+3 (k4 % 4 == 0)
+  auto load_b = [&](int c, uint32_t k4) -> f32x4t {
+    if constexpr (BLD == B_FC) {
+      return ld4(rsb, oob_unless(k4 < kw1, bcol[c] + k4 * 4u));
+    } else {
+      f32x4t v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t k = k4 + q;
+        if constexpr (BLD == B_IM1X1) {
+          v[q] = ld1(rsb, oob_unless(k < kw1, bcol[c] + k * p.HW * 4u));
+        } else {
+          const uint32_t ic = fdiv(k, p.kyx_m, p.kyx_s), rem = k - ic * p.KYX;
+          const uint32_t ky = fdiv(rem, p.kx_m, p.kx_s), kx = rem - ky * p.KX;
+          const bool ok = (k < kw1) & ((uint32_t)(iy0[c] + (int)ky) < p.H) & ((uint32_t)(ix0[c] + (int)kx) < p.W);
+          v[q] = ld1(rsb, oob_unless(ok, (bcol[c] + ic * p.HW + ky * p.W + kx) * 4u));
+        }
+      }
+      return v;
+    }
+  };
+
+  f32x4t acc[R][C];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[r][c] = f32x4t{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // K batches of KB: all of a batch's loads are issued before its MFMAs
+  f32x4t a0[NG][R], b0[NG][C], a1[DB ? NG : 1][R], b1[DB ? NG : 1][C];
+  auto load_batch = [&](uint32_t kb, f32x4t(&a)[NG][R], f32x4t(&b)[NG][C]) {
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg) {
+      const uint32_t k4 = kb + 16 * gg + 4 * g;
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[gg][r] = ld4(rsa, oob_unless(k4 < kw1, arow[r] + k4 * 4u));
+#pragma unroll
+      for (int c = 0; c < C; ++c) b[gg][c] = load_b(c, k4);
+    }
+  };
+  auto mma_batch = [&](const f32x4t(&a)[NG][R], const f32x4t(&b)[NG][C]) {
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[gg][r][q], b[gg][c][q], acc[r][c], 0, 0, 0);
+  };
+  uint32_t kb = kw0;
+  if constexpr (DB) {
+    if (kb < kw1) load_batch(kb, a0, b0);
+    while (kb < kw1) {
+      const uint32_t k1 = kb + KB;
+      if (k1 < kw1) load_batch(k1, a1, b1);
+      mma_batch(a0, b0);
+      if (k1 >= kw1) break;
+      const uint32_t k2 = k1 + KB;
+      if (k2 < kw1) load_batch(k2, a0, b0);
+      mma_batch(a1, b1);
+      kb = k2;
+    }
+  } else {
+    for (; kb < kw1; kb += KB) {
+      load_batch(kb, a0, b0);
+      mma_batch(a0, b0);
+    }
+  }
+
+  // ---- the NW waves' partial tiles -> LDS (row-major BMr x NC), summed in wave order.
+  // 16x16x4 C/D map: register j of lane l is row 4 * (l >> 4) + j, column l & 15.
+  {
+    float *const Rw = red + wave * TSZ;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Rw[(16 * r + 4 * g + j) * NC + 16 * c + i] = acc[r][c][j];
+  }
+  __syncthreads();
+  const bool has = NCH % NT == 0 || tid < NCH;
+  f32x4v v[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int ch = has ? tid + j * NT : 0;
+    v[j] = *(const f32x4v *)&red[4 * ch];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v[j] += *(const f32x4v *)&red[w * TSZ + 4 * ch];
+  }
+  constexpr int IMODE = 1;
+  if (gridDim.y == 1) {
+    if (has) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) finish_store<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], nullptr);
+    }
+    return;
+  }
+  // ---- K chunks: slab [split][tile][TSZ] (write-through), ticket, last arriver combines
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)split * p.tiles_m * p.tiles_n + tile) * TSZ, TSZ * 4);
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]),
+                                             rw, 16 * (tid + j * NT), 0, AUX_SC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
+    if (last) __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+  combine_tile<IMODE, NT, CH, CH, NCH>(p, tile, tm, tn, gridDim.y, nullptr, tid);
+}
+
+template <int R, int C, int NW, int NG, int DB>
+cfg_t gv_cfg(const char *name) {
+  cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 0};  // BK: K granule of a block chunk
+  c.gv = 1;
+  c.k[A_MVEC][B_FC][0] = gv_kernel<R, C, NW, NG, DB, B_FC>;
+  c.k[A_MVEC][B_IM1X1][0] = gv_kernel<R, C, NW, NG, DB, B_IM1X1>;
+  c.k[A_MVEC][B_IM2COL][0] = gv_kernel<R, C, NW, NG, DB, B_IM2COL>;
+  return c;
+}
+
+}  // namespace
+
+std::vector<cfg_t> gv_cfgs() {
+  return {
+      // filter streaming (few columns, big banks)
+      gv_cfg<4, 1, 4, 4, 1>("gv64x16"),
+      gv_cfg<4, 2, 4, 4, 1>("gv64x32"),
+      gv_cfg<2, 4, 4, 4, 1>("gv32x64"),
+      gv_cfg<2, 2, 4, 4, 1>("gv32x32"),
+      // latency configurations for small ops: 8 or 16 waves split K inside a block, so the
+      // whole K of a small op is in flight in one or two memory round trips
+      gv_cfg<2, 2, 8, 4, 1>("gv32x32w8"),
+      gv_cfg<2, 2, 16, 2, 0>("gv32x32w16"),
+      gv_cfg<4, 2, 8, 2, 1>("gv64x32w8"),
+      gv_cfg<2, 4, 8, 2, 1>("gv32x64w8"),
+      gv_cfg<4, 4, 8, 2, 0>("gv64x64w8"),
+      gv_cfg<4, 4, 4, 2, 0>("gv64x64"),
+  };
+}
+
+}  // namespace bhk

@@ -185,23 +185,38 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   // The next stage's DMAs (into slot islot) are issued between the MFMA steps, so their
   // issue cycles hide under MFMA execution instead of delaying the first MFMA.
   constexpr int S2 = BK / 2;
+  constexpr int PF = TM * TN >= 4 ? 1 : 2;  // LDS fragment prefetch distance (k steps)
   auto compute = [&](int slot, int islot, uint32_t k0) {
     uint32_t vo[LW];
     plan_stage(k0, vo);
     const float *const Ab = smem + slot * SLOT + kh * S2 * BM + wm * WM + TM * li;
     const float *const Bb = smem + slot * SLOT + A_LDS + kh * S2 * BN + wn * WN + TN * li;
+    // fragments of step s+PF are read while step s's MFMAs run (a ds_read waited for right
+    // before its MFMA leaves the SIMD idle for the LDS latency every step)
+    typename fvec<TM>::t av[PF + 1];
+    typename fvec<TN>::t bv[PF + 1];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      av[s] = *(const typename fvec<TM>::t *)&Ab[s * BM];
+      bv[s] = *(const typename fvec<TN>::t *)&Bb[s * BN];
+    }
 #pragma unroll
     for (int s = 0; s < S2; ++s) {
-      const typename fvec<TM>::t av = *(const typename fvec<TM>::t *)&Ab[s * BM];
-      const typename fvec<TN>::t bv = *(const typename fvec<TN>::t *)&Bb[s * BN];
+      if (s + PF < S2) {
+        av[(s + PF) % (PF + 1)] = *(const typename fvec<TM>::t *)&Ab[(s + PF) * BM];
+        bv[(s + PF) % (PF + 1)] = *(const typename fvec<TN>::t *)&Bb[(s + PF) * BN];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget<TM>(av, i), vget<TN>(bv, j), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget<TM>(av[s % (PF + 1)], i), vget<TN>(bv[s % (PF + 1)], j),
+                                                           acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < LW; ++q)
         if (q * S2 / LW == s) issue_one(q, islot, vo[q]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -341,6 +356,347 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Stream-K ring kernel: the ring above as a persistent grid. A launch has G blocks (one or
+// two per CU, whatever the LDS allows) and the op's work is the list of (output tile, K tile)
+// iterations, tile-major; logical block l takes iterations [l*ipb, (l+1)*ipb). Every CU does
+// the same number of MFMA steps whatever the tile count (no partial last wave of tiles),
+// and the DMA ring runs on across tile boundaries, so only the very first stage of a block
+// waits a full memory latency.
+//  * a tile whose iterations all fall in one block is finished in place (bias, ReLU, store);
+//  * a tile cut by block boundaries: each of its blocks writes its partial tile (write-through)
+//    to its own slab (slot 0: the block's first tile, slot 1: its last), takes the tile's
+//    ticket, and the last arriver sums the slabs in k order (block b0..b1) and stores -- the
+//    same fixed-order rule as the split-K combine, so results are bitwise reproducible.
+// Logical blocks are laid out XCD-contiguously (hardware deals blocks round-robin over the
+// 8 XCDs), so each XCD's L2 sees a contiguous run of tiles.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xcd_contig(uint32_t bid, uint32_t G) {
+  const uint32_t xcd = bid & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+// tile index -> (tile_m, tile_n), m fastest: consecutive tiles of a block share the B
+// (input) column panel, the big operand of a convolution
+__device__ __forceinline__ void sk_tile_coords(const GemmArgs &p, uint32_t t, uint32_t &tm, uint32_t &tn) {
+  tn = fdiv(t, p.tm_m, p.tm_s);
+  tm = t - tn * p.tiles_m;
+}
+
+template <int TM, int TN, int BK, int D, int BLD>
+__global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
+  constexpr int NW = 4, NT = 256;
+  constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1);
+  constexpr bool DW = IM;
+  static_assert(BLD == B_KVEC || DW, "stream-K loaders: SGEMM 16-B, conv im2col / 1x1 dword");
+  static_assert(NW % TN == 0, "a wave's B columns: one 64-column group");
+  constexpr int A_LDS = BK * BM, B_LDS = BK * BN, SLOT = A_LDS + B_LDS;
+  constexpr int LA = BK * BM / (NW * 256);
+  constexpr int LB = DW ? BK * TN / NW : BK * BN / (NW * 256);
+  static_assert(BK * BM % (NW * 256) == 0 && (DW ? BK * TN % NW : BK * BN % (NW * 256)) == 0,
+                "whole DMA instructions per wave");
+  constexpr int LW = LA + LB;
+  static_assert(LA >= 1 && LB >= 1 && D >= 2 && (D - 2) * LW <= 63, "vmcnt range");
+  constexpr int NCH = BM * BN / 4, CH = NCH / NT;  // float4 chunks of a tile, per thread
+  static_assert(NCH % NT == 0, "combine chunking");
+
+  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + 4];
+  uint32_t *const flag = (uint32_t *)(smem + D * SLOT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const uint32_t lb = xcd_contig(blockIdx.x, gridDim.x);
+  const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
+
+  constexpr int RA = 256 / BM, RB = 256 / BN;
+  const uint32_t bgrp = (uint32_t)(wave % TN);
+  const uint32_t rw0 = (uint32_t)(wave / TN);
+  constexpr uint32_t RSTEP = NW / TN;
+
+  // ---- per-lane DMA source state of the tile being issued, recomputed for every stage
+  // without branches (a branch around it made hipcc drain the DMA ring, vmcnt(0), at the
+  // K loop head; the recomputation is ~20 VALU + a few SALU per 32-deep K tile)
+  uint32_t a_lane = 0, b_lane = 0;
+  int col_base = 0, iy0 = 0, ix0 = 0;
+  auto set_tile = [&](uint32_t t) {
+    uint32_t tm, tn;
+    sk_tile_coords(p, t, tm, tn);
+    const uint32_t bm0 = tm * BM, bn0 = tn * BN;
+    const uint32_t am = bm0 + (uint32_t)(4 * lane) % BM;
+    a_lane = oob_unless(am < p.M, ((uint32_t)(4 * lane) / BM * p.lda + am) * 4u);
+    if constexpr (BLD == B_KVEC) {
+      const uint32_t bn = bn0 + (uint32_t)(4 * lane) % BN;
+      b_lane = oob_unless(bn < p.N, ((uint32_t)(4 * lane) / BN * p.ldb + bn) * 4u);
+    } else {
+      const uint32_t col = bn0 + bgrp * 64 + (uint32_t)lane;
+      const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
+      const uint32_t pix = col - img * p.OHW;
+      if constexpr (BLD == B_IM1X1) {
+        col_base = col < p.N ? (int)(img * p.ICHW + pix) * 4 : (int)OOB;
+      } else {
+        const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s);
+        const uint32_t ox = pix - oy * p.OW;
+        iy0 = (int)(oy * p.sy) - (int)p.py;
+        ix0 = (int)(ox * p.sx) - (int)p.px;
+        col_base = (int)(img * p.ICHW) + iy0 * (int)p.W + ix0;
+        if (col >= p.N) iy0 = -(1 << 29);
+      }
+    }
+  };
+  auto tap_off = [&](uint32_t kyx) -> uint32_t {
+    const uint32_t ky = fdiv(kyx, p.kx_m, p.kx_s), kx = kyx - ky * p.KX;
+    const bool ok = (kyx < p.KYX) & ((uint32_t)(iy0 + (int)ky) < p.H) & ((uint32_t)(ix0 + (int)kx) < p.W);
+    return oob_unless(ok, (uint32_t)(col_base + (int)(ky * p.W + kx)) * 4u);
+  };
+  // source offsets of this wave's LW DMA instructions for iteration `it` (all OOB past it1)
+  auto plan_stage = [&](uint32_t it, uint32_t(&vo)[LW]) {
+    const bool live = it < it1;
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    set_tile(t);
+    const uint32_t k0 = (it - t * p.ipt) * BK;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) vo[j] = a_lane + (k0 + RA * (wave * LA + j)) * p.lda * 4u;
+    if constexpr (BLD == B_KVEC) {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) vo[LA + j] = b_lane + (k0 + RB * (wave * LB + j)) * p.ldb * 4u;
+    } else if constexpr (BLD == B_IM1X1) {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const uint32_t k = k0 + rw0 + RSTEP * j;
+        vo[LA + j] = (uint32_t)col_base + (k < p.K ? k * p.HW * 4u : 0x40000000u);
+      }
+    } else if constexpr (BLD == B_IMT2) {
+      const uint32_t kf = k0 + rw0;
+      const uint32_t kyx = fdiv(kf, p.ic_m, p.ic_s);
+      const uint32_t ic0 = kf - kyx * p.IC;
+      const uint32_t t0 = tap_off(kyx), t1 = tap_off(kyx + 1);
+      const uint32_t hw4 = p.HW * 4u, ichw4 = p.IC * hw4;
+      uint32_t soff = ic0 * hw4;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const bool nxt = ic0 + RSTEP * j >= p.IC;
+        vo[LA + j] = (nxt ? t1 : t0) + (nxt ? soff - ichw4 : soff);
+        soff += RSTEP * hw4;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const uint32_t k = k0 + rw0 + RSTEP * j;
+        const uint32_t kyx = fdiv(k, p.ic_m, p.ic_s);
+        const uint32_t ic = k - kyx * p.IC;
+        vo[LA + j] = tap_off(kyx) + ic * p.HW * 4u;
+      }
+    }
+    // dead stages: set the top offset bit (a miss) -- a select, not a branch (a branch here
+    // made hipcc wait vmcnt(0) at the join)
+    const uint32_t dead = live ? 0u : OOB;
+#pragma unroll
+    for (int q = 0; q < LW; ++q) vo[q] |= dead;
+  };
+  auto issue_one = [&](int q, int slot, uint32_t vo) {
+    float *const Ab = smem + slot * SLOT;
+    float *const Bb = Ab + A_LDS;
+    if (q < LA) {
+      dma16(rsa, Ab + (wave * LA + q) * 256, vo);
+    } else if constexpr (BLD == B_KVEC) {
+      dma16(rsb, Bb + (wave * LB + q - LA) * 256, vo);
+    } else {
+      dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  };
+
+  const int kh = lane >> 5, li = lane & 31;
+  constexpr int S2 = BK / 2;
+  constexpr int PF = TM * TN >= 4 ? 1 : 2;
+  auto compute = [&](int slot, int islot, uint32_t it_issue) {
+    uint32_t vo[LW];
+    plan_stage(it_issue, vo);
+    const float *const Ab = smem + slot * SLOT + kh * S2 * BM + wm * WM + TM * li;
+    const float *const Bb = smem + slot * SLOT + A_LDS + kh * S2 * BN + wn * WN + TN * li;
+    typename fvec<TM>::t av[PF + 1];
+    typename fvec<TN>::t bv[PF + 1];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      av[s] = *(const typename fvec<TM>::t *)&Ab[s * BM];
+      bv[s] = *(const typename fvec<TN>::t *)&Bb[s * BN];
+    }
+#pragma unroll
+    for (int s = 0; s < S2; ++s) {
+      if (s + PF < S2) {
+        av[(s + PF) % (PF + 1)] = *(const typename fvec<TM>::t *)&Ab[(s + PF) * BM];
+        bv[(s + PF) % (PF + 1)] = *(const typename fvec<TN>::t *)&Bb[(s + PF) * BN];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget<TM>(av[s % (PF + 1)], i), vget<TN>(bv[s % (PF + 1)], j),
+                                                           acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < LW; ++q)
+        if (q * S2 / LW == s) issue_one(q, islot, vo[q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // finished tile t: this block's accumulators hold iterations [max(it0, t*ipt), min(it1, (t+1)*ipt))
+  auto finish_tile = [&](uint32_t t) {
+    uint32_t tm, tn;
+    sk_tile_coords(p, t, tm, tn);
+    const uint32_t bm0 = tm * BM, bn0 = tn * BN;
+    const uint32_t tb = t * p.ipt;
+    if (tb >= it0 && tb + p.ipt <= it1) {
+      // whole tile here: bias, ReLU, store
+      const uint32_t n_base = bn0 + wn * WN + TN * li;
+      int cofs[TN];
+      if constexpr (IM) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const uint32_t col = n_base + j;
+          const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
+          cofs[j] = col < p.N ? (int)(img * p.OCOHW + (col - img * p.OHW)) : -1;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t m = bm0 + wm * WM + TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+          if (m >= p.M) continue;
+          const float bias = (IM && p.bias) ? p.bias[m] : 0.0f;
+          float v[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const float x = acc[i][j][r] + bias;
+            v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
+          }
+          if constexpr (IM) {
+            float *const crow = p.c + (size_t)m * p.OHW;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              if (cofs[j] >= 0) crow[cofs[j]] = v[j];
+          } else {
+            float *const crow = p.c + (size_t)m * p.ldc + n_base;
+            if (p.cvec && n_base + TN <= p.N) {
+              typename fvec<TN>::t w;
+              if constexpr (TN == 1) w = v[0]; else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j) w[j] = v[j];
+              }
+              *(typename fvec<TN>::t *)crow = w;
+            } else {
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                if (n_base + j < p.N) crow[j] = v[j];
+            }
+          }
+        }
+      }
+      return;
+    }
+    // partial tile: slab (block, slot), ticket, the last arriver combines in k order
+    const uint32_t slot = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
+    float *const wz = p.ws + ((size_t)lb * 2 + slot) * (BM * BN);
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(wz, BM * BN * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * WM + TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+        const uint32_t off = row * BN + wn * WN + TN * li;
+        typename fvec<TN>::t w;
+        if constexpr (TN == 1) w = acc[i][0][r]; else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
+        }
+        if constexpr (TN == 1) {
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, w), rw, off * 4, 0, AUX_SC1);
+        } else if constexpr (TN == 2) {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) uint32_t, w),
+                                                rw, off * 4, 0, AUX_SC1);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, w),
+                                                 rw, off * 4, 0, AUX_SC1);
+        }
+      }
+    const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == b1 - b0 ? 1u : 0u;
+      if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+    const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+    f32x4v sum[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t b = b0; b <= b1; ++b) {
+      const uint32_t sl = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+      const uint32_t base = (b * 2 + sl) * (uint32_t)(BM * BN * 4);
+      f32x4v x[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        x[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rall, base + 16 * (tid + j * NT), 0,
+                                                                                 AUX_SC1));
+#pragma unroll
+      for (int j = 0; j < CH; ++j) sum[j] += x[j];
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) finish_store<IM ? 1 : 0>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], nullptr);
+  };
+
+  // ---- main loop over this block's iterations: D-stage ring running across tiles
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) {
+    uint32_t vo[LW];
+    plan_stage(it0 + s, vo);
+#pragma unroll
+    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+  }
+  // outer loop over this block's tiles, inner loop over a tile's K iterations (a nested
+  // loop keeps the accumulators in AGPRs: a flat loop with the tile epilogue inside made
+  // hipcc copy them VGPR <-> AGPR around every K tile)
+  int slot = 0;
+  uint32_t it = it0;
+  while (it < it1) {
+    const uint32_t ct = fdiv(it, p.ipt_m, p.ipt_s);   // tile being accumulated
+    const uint32_t ct_end = min(it1, (ct + 1) * p.ipt);
+    zero_acc();
+    for (; it < ct_end; ++it) {
+      vm_wait<(D - 2) * LW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(slot, slot == 0 ? D - 1 : slot - 1, it + D - 1);
+      slot = slot == D - 1 ? 0 : slot + 1;
+    }
+    finish_tile(ct);
+    // a real (compiler-visible) vmcnt(0) after the tile's stores: otherwise hipcc carries the
+    // epilogue's pending stores into the K loop head and waits vmcnt(0) there every iteration
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+  vm_wait<0>();
+}
+
 // Filter-bank repack for the ring conv kernels: wp[(kyx * IC + ic)][m] = w[m][ic * KYX + kyx]
 // for m < OC (K order (ky, kx, ic): one tap per run of IC rows), 0 for OC <= m < OC4 (rows
 // padded to a multiple of 4 floats for 16-B DMA) and for rows K <= k < Kp (K padded to a
@@ -383,6 +739,20 @@ cfg_t ring_conv_cfg(const char *name) {
   return c;
 }
 template <int TM, int TN, int BK, int D>
+cfg_t srk_conv_cfg(const char *name) {
+  cfg_t c{name, 64 * TM, 64 * TN, BK, 256, {}, 1, 1, (D * BK * 64 * (TM + TN) + 4) * 4};
+  c.k[A_KVEC][B_IM2COL][0] = srk_kernel<TM, TN, BK, D, B_IM2COL>;
+  c.k[A_KVEC][B_IMT2][0] = srk_kernel<TM, TN, BK, D, B_IMT2>;
+  c.k[A_KVEC][B_IM1X1][0] = srk_kernel<TM, TN, BK, D, B_IM1X1>;
+  return c;
+}
+template <int TM, int TN, int BK, int D>
+cfg_t srk_sgemm_cfg(const char *name) {
+  cfg_t c{name, 64 * TM, 64 * TN, BK, 256, {}, 0, 1, (D * BK * 64 * (TM + TN) + 4) * 4};
+  c.k[A_KVEC][B_KVEC][0] = srk_kernel<TM, TN, BK, D, B_KVEC>;
+  return c;
+}
+template <int TM, int TN, int BK, int D>
 cfg_t ring_sgemm_cfg(const char *name) {
   cfg_t c{name, 64 * TM, 64 * TN, BK, 256, {}, 0};
   reg_ring<TM, TN, BK, D, B_KVEC>(c);
@@ -399,6 +769,10 @@ std::vector<cfg_t> ring_cfgs(int op) {
         ring_sgemm_cfg<2, 2, 64, 2>("r128x128x64d2"),
         ring_sgemm_cfg<2, 2, 32, 2>("r128x128x32d2"),
         ring_sgemm_cfg<2, 4, 32, 3>("r128x256x32d3"),
+        srk_sgemm_cfg<2, 2, 32, 2>("srk128x128x32d2"),
+        srk_sgemm_cfg<2, 2, 16, 4>("srk128x128x16d4"),
+        srk_sgemm_cfg<2, 2, 32, 4>("srk128x128x32d4"),
+        srk_sgemm_cfg<2, 2, 32, 3>("srk128x128x32d3"),
     };
   return {
       ring_conv_cfg<2, 2, 32, 4>("r128x128x32d4"),
@@ -414,6 +788,16 @@ std::vector<cfg_t> ring_cfgs(int op) {
       ring_conv_cfg<2, 1, 32, 3>("r128x64x32d3"),
       ring_conv_cfg<1, 2, 32, 3>("r64x128x32d3"),
       ring_conv_cfg<1, 4, 32, 2>("r64x256x32d2"),
+      srk_conv_cfg<2, 2, 32, 2>("srk128x128x32d2"),
+      srk_conv_cfg<2, 2, 16, 4>("srk128x128x16d4"),
+      srk_conv_cfg<2, 2, 32, 4>("srk128x128x32d4"),
+      srk_conv_cfg<2, 2, 32, 3>("srk128x128x32d3"),
+      srk_conv_cfg<2, 1, 32, 4>("srk128x64x32d4"),
+      srk_conv_cfg<2, 1, 32, 3>("srk128x64x32d3"),
+      srk_conv_cfg<1, 2, 32, 4>("srk64x128x32d4"),
+      srk_conv_cfg<1, 2, 32, 3>("srk64x128x32d3"),
+      srk_conv_cfg<1, 1, 32, 4>("srk64x64x32d4"),
+      srk_conv_cfg<1, 4, 32, 3>("srk64x256x32d3"),
   };
 }
 

@@ -80,3 +80,73 @@ def test_split_k_repeatable(dev):
 def test_tune_set_rejects_unknown_config(dev):
     with pytest.raises(boda_hip.UnsupportedError):
         dev.tune_set(1, 1000, 0)
+
+
+# Stream-K configurations (srk*: persistent grid, iterations dealt equally to blocks) on
+# shapes whose blocks finish whole tiles in place AND share cut tiles through slabs.
+SRK_CONV_SHAPES = [
+    ops.ConvShape(16, 64, 64, 64, 100, 1, 1, 1, 1, 0, 0),  # 1x1, K = 64: several whole tiles per block
+    ops.ConvShape(2, 64, 30, 30, 96, 3, 3, 1, 1, 1, 1),    # two-tap loader, every tile cut
+    ops.ConvShape(2, 3, 50, 50, 64, 7, 7, 2, 2, 3, 3),     # IC < BK stem conv, stride 2
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("srk")])
+@pytest.mark.parametrize("bpc", [1, 2])
+def test_conv_streamk(dev, cn, bpc):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), bpc)
+    try:
+        for s in SRK_CONV_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            ref = orc.conv_ref(i, f, b, s, 1)
+            nm, rl2, _ = orc.normalized_errors(ref, out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            # fixed-order slab combine: bitwise repeatable
+            np.testing.assert_array_equal(run_conv(dev, s), out)
+    finally:
+        dev.tune_set(1, -1, 0)
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(0) if n.startswith("srk")])
+@pytest.mark.parametrize("bpc", [1, 2])
+def test_sgemm_streamk(dev, cn, bpc):
+    dev.tune_set(0, boda_hip.tune_cfg_names(0).index(cn), bpc)
+    try:
+        for M, N, K in [(2048, 1024, 96), (1000, 1000, 1000), (384, 260, 2048)]:
+            out = run_sgemm(dev, M, N, K, 600).reshape(M, N)
+            np.testing.assert_array_equal(out, kat_expect(M, N, K))
+        out = run_sgemm(dev, 640, 384, 700, 5)
+        a, b = orc.gen_sgemm(640, 384, 700, 5)
+        nm, rl2, _ = orc.normalized_errors(orc.sgemm_ref(a, b, 640, 384, 700), out)
+        assert nm <= 1e-4 and rl2 <= 1e-5
+    finally:
+        dev.tune_set(0, -1, 0)
+
+
+# Filter-streaming configurations (gv*: few output columns, bank read in its reference layout)
+GV_SHAPES = [
+    ops.ConvShape(5, 64, 6, 6, 300, 6, 6, 1, 1, 0, 0),    # fc-as-conv: window = input (B_FC), 5 columns
+    ops.ConvShape(3, 520, 1, 1, 130, 1, 1, 1, 1, 0, 0),   # InnerProduct on 1x1 input (B_FC), ragged M
+    ops.ConvShape(1, 96, 6, 6, 70, 1, 1, 1, 1, 0, 0),     # 1x1, 36 columns (B_IM1X1)
+    ops.ConvShape(1, 40, 6, 6, 100, 3, 3, 1, 1, 1, 1),    # 3x3 pad 1, 36 columns (B_IM2COL)
+    ops.ConvShape(2, 12, 5, 5, 33, 3, 3, 2, 2, 0, 0),     # stride 2, 8 columns
+    ops.ConvShape(2, 48, 14, 14, 70, 3, 3, 1, 1, 1, 1),   # 392 columns: a 2-D tile grid
+    ops.ConvShape(1, 200, 7, 7, 40, 1, 1, 1, 1, 0, 0),    # 1x1, 49 columns, K % 16 != 0
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gv")])
+@pytest.mark.parametrize("splits", [0, 1, 5])
+def test_conv_gv(dev, cn, splits):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
+    try:
+        for s in GV_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            ref = orc.conv_ref(i, f, b, s, 1)
+            nm, rl2, _ = orc.normalized_errors(ref, out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed-order combine
+    finally:
+        dev.tune_set(1, -1, 0)

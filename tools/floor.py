@@ -40,6 +40,24 @@ def main():
     with bh.Device(0) as dev:
         tiny = dev.alloc_floats(64)
         res["gen_data_4"] = timed(dev, lambda: dev.gen_data(bh.GEN_CONV_BIASES, tiny, [4], 5), args.reps)
+        # back-to-back floor inside a replayed graph: stamp kernels only (one lane each),
+        # and tiny gen_data calls between stamps
+        for label, body in (("graph: stamp->stamp", None),
+                            ("graph: gen_data_4 between stamps", lambda: dev.gen_data(bh.GEN_CONV_BIASES, tiny, [4], 5))):
+            n = 100
+            dev.capture_begin()
+            for j in range(n + 1):
+                dev.stamp(j)
+                if body is not None and j < n:
+                    body()
+            g = dev.capture_end()
+            per = []
+            for _ in range(5):
+                dev.graph_launch(g)
+                t = dev.stamps_read(0, n + 1)
+                per.append((t[n] - t[0]) / n)
+            dev.graph_destroy(g)
+            res[label] = {"median_us": statistics.median(per), "min_us": min(per), "mean_us": statistics.fmean(per)}
         shapes = [ConvShape(*map(int, s.split())) for s in args.shapes.split(";")]
         wl = Workload(dev, shapes)
         for i, s in enumerate(shapes):

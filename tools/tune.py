@@ -37,6 +37,8 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
+    if name.startswith("gv"):
+        return 16 * (int(name.split("w")[1]) if "w" in name else 4)
     return int(re.match(r"\d+", name.split("x")[2]).group(0))
 
 
@@ -124,6 +126,14 @@ def main():
             if not (kind == 0 and s.flops() > args.max_flop_sgemm):
                 for ci, cn in enumerate(names[kind]):
                     nkt = -(-K // bk_of(cn))
+                    if cn.startswith("srk"):  # stream-K: S = blocks per CU
+                        cand += [(ci, 1), (ci, 2)]
+                        continue
+                    if cn.startswith("gv"):  # register-streaming kernels: S = K chunks
+                        tiles = -(-M // int(cn[2:].split("x")[0])) * -(-N // int(cn.split("x")[1].split("w")[0]))
+                        if tiles <= 512:
+                            cand += [(ci, S) for S in [0] + SPLITS if S == 0 or nkt >= S]
+                        continue
                     for S in SPLITS:
                         if S > 1 and nkt < 2 * S:
                             continue
