@@ -953,6 +953,7 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
   p.tbm = c.BM;
   p.tbn = c.BN;
+  if (bld == B_IMTAB && !c.k[ald][bld][0]) bld = B_IM2COL;  // table loader: ring kernels only
   if (c.gv) {
     // filter-streaming kernel (bh_gv.hip): one block per (64-row tile, K chunk); the K chunks
     // of a tile are combined by its last arriver. ch.splits = K chunks (0: ~1024 blocks)
@@ -1024,7 +1025,8 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
     if (rc != BH_OK) return rc;
     const uint64_t total = nblk * c.BM * c.BN / 4;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
-    const void *rk = (bld == B_IM2COL || bld == B_IMT2 || bld == B_IM1X1 || bld == B_IM1X1V) ? (const void *)splitk_reduce_kernel<1>
+    const void *rk = (bld == B_IM2COL || bld == B_IMT2 || bld == B_IM1X1 || bld == B_IM1X1V || bld == B_IMTAB)
+                         ? (const void *)splitk_reduce_kernel<1>
                                                           : (const void *)splitk_reduce_kernel<0>;
     uint32_t Sv = S;
     void *rargs[] = {&p, &Sv};
@@ -1172,7 +1174,9 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       p.a_bytes = kp * oc4 * 4;
       p.IC = IC;
       set_fd(IC, p.ic_m, p.ic_s);
-      return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1 : (IC >= (uint32_t)cfgs(1)[ch.cfg].BK ? B_IMT2 : B_IM2COL), p,
+      const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
+      const bool tab = ((p.K + bk - 1) / bk) * bk + 3 * bk <= (uint32_t)TAB_MAX;  // rows a block tabulates
+      return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1 : (IC >= bk ? B_IMT2 : (tab ? B_IMTAB : B_IM2COL)), p,
                          "conv", packed != nullptr);
     }
   }

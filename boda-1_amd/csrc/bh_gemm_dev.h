@@ -11,7 +11,11 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
-enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, NBLD = 7 };
+enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, B_IMTAB = 7, NBLD = 8 };
+// B_IMTAB: ring kernels' im2col for IC < BK (stem convs): the per-k-row (ic, ky, kx) decomposition
+// is tabulated in LDS once per block (TAB_MAX rows) instead of computed by scalar divisions
+// for every row of every stage
+constexpr int TAB_MAX = 512;
 // B_FC: the im2col of a conv whose window covers the whole (unpadded) input -- Boda's ipconv /
 // InnerProduct-as-conv -- is the input itself: column n = image n, X[k][n] = in[n * K + k]
 // B_IMT2: ring kernels' im2col when IC >= BK: a wave's rows of one K tile touch at most two
@@ -113,13 +117,13 @@ __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
 // Bias, ReLU and store of one float4 chunk c (tile elements 4c..4c+3, row-major BM x BN)
 // of tile (tile_m, tile_n): dense C rows, or NCHW scatter for conv (IMODE). p.cvec: rows
 // take aligned float4 stores (dense: ldc % 4 == 0; conv: OH*OW % 4 == 0).
+// finish_store_b: the same with the chunk's bias value already in hand (prefetched)
 template <int IMODE>
-__device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
-                                             f32x4v sum, const float *bias_lds) {
+__device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
+                                               f32x4v sum, float b) {
   const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
   const uint32_t m = tile_m * p.tbm + row;
   if (m >= p.M) return;
-  const float b = bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f);
   const uint32_t n0 = tile_n * p.tbn + col0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -148,6 +152,14 @@ __device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m,
       p.c[(size_t)m * p.ldc + n] = sum[t];
     }
   }
+}
+
+template <int IMODE>
+__device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
+                                             f32x4v sum, const float *bias_lds) {
+  const uint32_t row = 4 * c / p.tbn, m = tile_m * p.tbm + row;
+  if (m >= p.M) return;
+  finish_store_b<IMODE>(p, tile_m, tile_n, c, sum, bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f));
 }
 
 constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)

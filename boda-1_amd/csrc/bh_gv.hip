@@ -40,6 +40,7 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  KT(0);
   const uint32_t tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m, split = blockIdx.y;
   const uint32_t tile = blockIdx.x;
   const uint32_t m0 = tm * BMr;
@@ -103,6 +104,16 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
     }
   };
 
+  // bias of the rows this thread stores in the epilogue, fetched now (a dependent global
+  // load at the end of a small op costs a full memory round trip)
+  const bool has = NCH % NT == 0 || tid < NCH;
+  float bias_r[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const uint32_t m = m0 + 4 * (uint32_t)(tid + j * NT) / NC;
+    bias_r[j] = (has && p.bias && m < p.M) ? p.bias[m] : 0.0f;
+  }
+
   f32x4t acc[R][C];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -139,6 +150,7 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
       const uint32_t k1 = kb + KB;
       if (k1 < kw1) load_batch(k1, a1, b1);
       mma_batch(a0, b0);
+      if (kb == kw0) KT(1);
       if (k1 >= kw1) break;
       const uint32_t k2 = k1 + KB;
       if (k2 < kw1) load_batch(k2, a0, b0);
@@ -149,9 +161,11 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
     for (; kb < kw1; kb += KB) {
       load_batch(kb, a0, b0);
       mma_batch(a0, b0);
+      if (kb == kw0) KT(1);
     }
   }
 
+  KT(2);
   // ---- the NW waves' partial tiles -> LDS (row-major BMr x NC), summed in wave order.
   // 16x16x4 C/D map: register j of lane l is row 4 * (l >> 4) + j, column l & 15.
   {
@@ -164,7 +178,6 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
         for (int j = 0; j < 4; ++j) Rw[(16 * r + 4 * g + j) * NC + 16 * c + i] = acc[r][c][j];
   }
   __syncthreads();
-  const bool has = NCH % NT == 0 || tid < NCH;
   f32x4v v[CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) {
@@ -177,8 +190,12 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
   if (gridDim.y == 1) {
     if (has) {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) finish_store<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], nullptr);
+      for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], bias_r[j]);
     }
+#ifdef BH_KTRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KT(4);
+#endif
     return;
   }
   // ---- K chunks: slab [split][tile][TSZ] (write-through), ticket, last arriver combines
@@ -200,7 +217,24 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
   __syncthreads();
   if (!*flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
-  combine_tile<IMODE, NT, CH, CH, NCH>(p, tile, tm, tn, gridDim.y, nullptr, tid);
+  // the K chunks' slabs summed in chunk order (as combine_tile), all loads of a slab in flight
+  if (!has) return;
+  const uint32_t tstep = TSZ * p.tiles_m * p.tiles_n * 4;
+  const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+  f32x4v sum[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t q = 0; q < gridDim.y; ++q) {
+    f32x4v x[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      x[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rall, q * tstep + (tile * TSZ + 4 * (uint32_t)(tid + j * NT)) * 4, 0, AUX_SC1));
+#pragma unroll
+    for (int j = 0; j < CH; ++j) sum[j] += x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);
 }
 
 template <int R, int C, int NW, int NG, int DB>
@@ -230,6 +264,11 @@ std::vector<cfg_t> gv_cfgs() {
       gv_cfg<2, 4, 8, 2, 1>("gv32x64w8"),
       gv_cfg<4, 4, 8, 2, 0>("gv64x64w8"),
       gv_cfg<4, 4, 4, 2, 0>("gv64x64"),
+      // small output tiles: more blocks (CUs) share a small op's loads
+      gv_cfg<1, 1, 4, 4, 1>("gv16x16"),
+      gv_cfg<1, 1, 8, 4, 1>("gv16x16w8"),
+      gv_cfg<1, 2, 8, 4, 1>("gv16x32w8"),
+      gv_cfg<2, 1, 8, 4, 1>("gv32x16w8"),
   };
 }
 

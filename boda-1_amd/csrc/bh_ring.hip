@@ -29,7 +29,8 @@ template <int TM, int TN, int BK, int D, int BLD, int SPL>
 __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr int NW = 4, NT = 256;
   constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
-  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1);
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB);
+  constexpr int TABF = BLD == B_IMTAB ? 2 * TAB_MAX : 0;  // im2col row table (int2 per k row)
   constexpr bool DW = IM || BLD == B_KSCALAR;  // B by dword DMA: one k row x 64 columns per instruction
   static_assert(BLD == B_KVEC || DW, "ring loaders: k-major 16-B or dword (SGEMM b), im2col / 1x1 dword");
   static_assert(NW % TN == 0, "a wave's B columns: one 64-column group");
@@ -46,8 +47,9 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr int NBI = IM && SPL != 1 ? BM / 64 : 0;  // bias DMA instructions (wave 0)
 
   // one __shared__ array only (a second object makes hipcc wait vmcnt(0) at ds_reads)
-  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + (IM ? BM : 0) + 4];
+  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + (IM ? BM : 0) + 4 + TABF];
   float *const Lbias = smem + D * SLOT;
+  constexpr int TAB0 = D * SLOT + (IM ? BM : 0) + 4;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,6 +144,18 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
         vo[LA + j] = (nxt ? t1 : t0) + (nxt ? soff - ichw4 : soff);
         soff += RSTEP * hw4;
       }
+    } else if constexpr (BLD == B_IMTAB) {
+      // tabulated rows: {ic*HW + ky*W + kx, ky | kx << 16} (rows past the range: ky = 0x7fff)
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const uint32_t r = k0 - kbeg + rw0 + RSTEP * j;
+        // float-typed reads (the ring's TBAA type: an int-typed read made hipcc wait vmcnt(0))
+        const int ex = __builtin_bit_cast(int, smem[TAB0 + 2 * r]);
+        const int ey = __builtin_bit_cast(int, smem[TAB0 + 2 * r + 1]);
+        const int ky = ey & 0xffff, kx = ey >> 16;
+        const bool ok = ((uint32_t)(iy0 + ky) < p.H) & ((uint32_t)(ix0 + kx) < p.W);
+        vo[LA + j] = oob_unless(ok, (uint32_t)(col_base + ex) * 4u);
+      }
     } else {
       // any IC: (tap, ic) of each row by division (scalar), the lane's tap offset per row
 #pragma unroll
@@ -232,6 +246,18 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
         dma4(rsbias, Lbias + 64 * j, oob_unless(m < p.M, m * 4u));
       }
     }
+  }
+  if constexpr (BLD == B_IMTAB) {
+    // this block's K rows kbeg .. kbeg + (nkt + D - 1) * BK (the host checks <= TAB_MAX)
+    for (uint32_t r = tid; r < (nkt + D - 1) * BK; r += NT) {
+      const uint32_t k = kbeg + r;
+      const uint32_t kyx = k / p.IC, ic = k - kyx * p.IC;
+      const uint32_t ky = kyx / p.KX, kx = kyx - ky * p.KX;
+      const bool valid = k < kend;
+      smem[TAB0 + 2 * r] = __builtin_bit_cast(float, valid ? (int)(ic * p.HW + ky * p.W + kx) : 0);
+      smem[TAB0 + 2 * r + 1] = __builtin_bit_cast(float, valid ? (int)(ky | (kx << 16)) : 0x7fff);
+    }
+    __syncthreads();
   }
   // Stages past the split's end are issued too (their lanes read OOB zeros without
   // touching memory), so every wave always has exactly D-2 stages in flight behind the
@@ -734,6 +760,7 @@ template <int TM, int TN, int BK, int D>
 cfg_t ring_conv_cfg(const char *name) {
   cfg_t c{name, 64 * TM, 64 * TN, BK, 256, {}, 1};
   reg_ring<TM, TN, BK, D, B_IM2COL>(c);
+  reg_ring<TM, TN, BK, D, B_IMTAB>(c);
   reg_ring<TM, TN, BK, D, B_IMT2>(c);
   reg_ring<TM, TN, BK, D, B_IM1X1>(c);
   return c;
