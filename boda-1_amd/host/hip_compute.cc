@@ -16,6 +16,7 @@
 //     and skips (src/rtc_prof.cc:287-296).
 #include <cstring>
 #include <memory>
+#include <set>
 
 #include "boda_hip.h"
 #include "op_desc.H"
@@ -99,10 +100,18 @@ struct hip_compute_t : public rtc_compute_t {
     bh_check(bh_memset0(ctx, v.buf.get(), v.dims.bytes()), "bh_memset0");
   }
 
+  // function kind: the name up to "__" (a net registers one function per layer, e.g.
+  // hip_conv__conv1, the way Boda's codegen names one function per op signature)
+  static std::string kind_of(std::string const &fn) {
+    size_t k = fn.find("__");
+    return k == std::string::npos ? fn : fn.substr(0, k);
+  }
   void compile(std::vector<rtc_func_info_t> const &fis, rtc_compile_opts_t const &) override {
+    static const std::set<std::string> kinds = {"hip_sgemm", "hip_conv",  "hip_xpose_filts", "hip_pool",
+                                                "hip_lrn",   "hip_relu",  "hip_copy",        "hip_affine",
+                                                "hip_eltwise", "hip_softmax"};
     for (auto const &fi : fis) {
-      bool known = fi.func_name == "hip_sgemm" || fi.func_name == "hip_conv" || fi.func_name == "hip_xpose_filts" ||
-                   fi.func_name.rfind("gen_data_", 0) == 0;
+      bool known = kinds.count(kind_of(fi.func_name)) || fi.func_name.rfind("gen_data_", 0) == 0;
       if (!known)
         unsup_err("be=hip runs the hand-written gfx950 kernels (hip_sgemm, hip_conv, gen_data_*); '" +
                   fi.func_name + "' would need CUCL JIT, which this backend does not provide");
@@ -138,12 +147,73 @@ struct hip_compute_t : public rtc_compute_t {
     // events on the call's own first/last kernel dispatch (no host launch latency)
     bh_check(bh_time_next_call(ctx, &ev.b, &ev.e), "bh_time_next_call");
     std::string const &fn = fi.func_name;
-    if (fn == "hip_sgemm") {
+    const std::string kind = kind_of(fn);
+    auto sc = [&](char const *n) -> uint32_t {
+      auto it = fi.op.scalars.find(n);
+      if (it == fi.op.scalars.end()) rt_err(fn + ": op lacks '" + n + "'");
+      return (uint32_t)it->second;
+    };
+    auto fv = [&](char const *n) -> float {
+      auto it = fi.op.str_vals.find(n);
+      if (it == fi.op.str_vals.end()) rt_err(fn + ": op lacks '" + n + "'");
+      return strtof(it->second.c_str(), nullptr);
+    };
+    auto nchw = [&](char const *an, uint32_t &B, uint32_t &C, uint32_t &H, uint32_t &W) {
+      dims_t const &d = arg_dims(rfc, an);
+      B = d.dsz("img"); C = d.dsz("chan"); H = d.dsz("y"); W = d.dsz("x");
+    };
+    if (kind == "hip_pool") {
+      uint32_t B, C, H, W, OB, OC_, OH, OW;
+      nchw("in", B, C, H, W);
+      nchw("out", OB, OC_, OH, OW);
+      const uint32_t ky = sc("ky"), kx = sc("kx"), sy = sc("sy"), sx = sc("sx"), py = sc("py"), px = sc("px");
+      if (OB != B || OC_ != C || OH != (uint32_t)bh_pool_out_size(H, ky, sy, py) ||
+          OW != (uint32_t)bh_pool_out_size(W, kx, sx, px))
+        rt_err(fn + ": out dims do not match the pooling geometry");
+      bh_check(bh_pool_fwd_nchw(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "out"), nullptr, B, C, H, W, ky, kx, sy, sx, py,
+                                px, (int)sc("avg")),
+               fn);
+    } else if (kind == "hip_lrn") {
+      uint32_t B, C, H, W;
+      nchw("in", B, C, H, W);
+      if (arg_dims(rfc, "out") != arg_dims(rfc, "in")) rt_err(fn + ": in / out dims differ");
+      bh_check(bh_lrn_fwd_nchw(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "out"), nullptr, B, C, H, W, sc("local_size"),
+                               fv("alpha"), fv("beta"), fv("k")),
+               fn);
+    } else if (kind == "hip_relu") {
+      bh_check(bh_relu_inplace(ctx, arg_ptr(rfc, "x"), arg_dims(rfc, "x").elems()), fn);
+    } else if (kind == "hip_copy") {  // channel slab copy: Concat / Split / Dropout-as-copy
+      uint32_t B, C, H, W, OB, OC_, OH, OW;
+      nchw("in", B, C, H, W);
+      nchw("out", OB, OC_, OH, OW);
+      const uint32_t ic0 = sc("ic0"), oc0 = sc("oc0"), nc = sc("nc");
+      if (B != OB || H != OH || W != OW || ic0 + nc > C || oc0 + nc > OC_) rt_err(fn + ": channel slab out of range");
+      bh_check(bh_chan_copy(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "out"), B, H * W, C, ic0, OC_, oc0, nc), fn);
+    } else if (kind == "hip_affine") {
+      uint32_t B, C, H, W;
+      nchw("in", B, C, H, W);
+      if (arg_dims(rfc, "out") != arg_dims(rfc, "in") || arg_dims(rfc, "scale").elems() != C ||
+          arg_dims(rfc, "shift").elems() != C)
+        rt_err(fn + ": affine dims");
+      bh_check(bh_chan_affine(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "out"), arg_ptr(rfc, "scale"),
+                              arg_ptr(rfc, "shift"), B, C, H * W, (int)sc("relu")),
+               fn);
+    } else if (kind == "hip_eltwise") {
+      dims_t const &a = arg_dims(rfc, "a");
+      if (arg_dims(rfc, "b") != a || arg_dims(rfc, "out") != a) rt_err(fn + ": eltwise dims differ");
+      bh_check(bh_eltwise(ctx, arg_ptr(rfc, "a"), arg_ptr(rfc, "b"), arg_ptr(rfc, "out"), a.elems(), (int)sc("op"),
+                          (int)sc("relu")),
+               fn);
+    } else if (kind == "hip_softmax") {
+      uint32_t B, C, H, W;
+      nchw("in", B, C, H, W);
+      bh_check(bh_softmax_chans(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "prob"), B, C, H, W), fn);
+    } else if (kind == "hip_sgemm") {
       dims_t const &a = arg_dims(rfc, "a"), &b = arg_dims(rfc, "b");
       uint32_t M = a.dsz("M"), K = a.dsz("K"), N = b.dsz("N");
       if (b.dsz("K") != K) rt_err("hip_sgemm: a/b K mismatch");
       bh_check(bh_sgemm_kmajor(ctx, arg_ptr(rfc, "a"), arg_ptr(rfc, "b"), arg_ptr(rfc, "c"), M, N, K), "hip_sgemm");
-    } else if (fn == "hip_conv") {
+    } else if (kind == "hip_conv") {
       conv_shape_t s = get_conv_shape(fi.op);
       auto r = fi.op.scalars.find("conv_has_relu");
       int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
@@ -152,7 +222,7 @@ struct hip_compute_t : public rtc_compute_t {
                                      arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
                                      s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
                "hip_conv");
-    } else if (fn == "hip_xpose_filts") {  // Boda's xpose_filts (test/rtc/xpose_filts.cucl) for hip_conv
+    } else if (kind == "hip_xpose_filts") {  // Boda's xpose_filts (test/rtc/xpose_filts.cucl) for hip_conv
       conv_shape_t s = get_conv_shape(fi.op);
       if (arg_dims(rfc, "filts_xp").elems() != bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX))
         rt_err("hip_xpose_filts: filts_xp has the wrong size");

@@ -1,0 +1,62 @@
+"""Full-net forward on the GPU (BASELINE config C4): the net
+executor (boda_hip_rtc_fwd: prototxt reader + conv_pipe_fwd_t over be=hip, every layer a
+hand-written kernel behind the C-ABI) against oracle/net.py, the CPU restatement running the
+same plan with the per-layer oracles, on the reference's own nets at batch 1.
+
+Bar: rel-L2 <= 1e-4 and max|d| / max(1, max|ref|) <= 1e-3 on the net output (fp32 rounding of
+up to ~70 stacked layers vs a double-accumulating CPU conv; the per-op bar is 1e-5 / 1e-4).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import net as onet
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "boda-1_amd", "bin", "boda_hip_rtc_fwd")
+NETS = os.path.join(ROOT, "tests", "golden", "nets")
+
+
+def run_net(net, img, tmp, extra=()):
+    pt = os.path.join(NETS, net + ".prototxt")
+    r = subprocess.run([BIN, "--net", pt, "--img", str(img), "--plan-json"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    plan = json.loads(r.stdout)
+    r = subprocess.run([BIN, "--net", pt, "--img", str(img), "--iters", "2", "--save", str(tmp)] + list(extra),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    print(r.stdout)
+    x = np.fromfile(os.path.join(tmp, "in.f32"), dtype=np.float32)
+    got = np.fromfile(os.path.join(tmp, "out.f32"), dtype=np.float32)
+    return plan, x, got, r.stdout
+
+
+@pytest.mark.parametrize("net", ["alexnet_ng_conv", "nin_imagenet", "googlenet_conv", "resnet-50", "vgg_19"])
+def test_net_forward(net, tmp_path):
+    plan, x, got, _ = run_net(net, 1, tmp_path)
+    d0 = plan["inputs"][0]["dims"]
+    np.testing.assert_array_equal(x, onet.det_hash_rand_vec(int(np.prod(d0)), onet.IN_SEED))
+    blobs = onet.forward(plan, x.reshape(d0))
+    ref = blobs[plan["out_node"]].reshape(-1)
+    assert ref.shape == got.shape
+    nm, rl2, _ = orc.normalized_errors(ref, got)
+    print(net, "out", plan["out_node"], "nm %.2e rl2 %.2e" % (nm, rl2))
+    assert rl2 <= 1e-4 and nm <= 1e-3, (net, nm, rl2)
+
+
+def test_net_unpacked_bank_same_bits(tmp_path):
+    """--no-pack (filter banks transformed inside every conv call) gives the same output bits."""
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _, _, g1, _ = run_net("alexnet_ng_conv", 2, a)
+    _, _, g2, _ = run_net("alexnet_ng_conv", 2, b, ["--no-pack"])
+    np.testing.assert_array_equal(g1, g2)

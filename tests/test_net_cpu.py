@@ -1,0 +1,84 @@
+"""Host logic of the net executor, no GPU: the prototxt reader and
+net plan of boda-1_amd/bin/boda_hip_rtc_fwd (--plan-json) on the reference's own nets
+(tests/golden/nets/, copied from the reference's nets/ directory as fixtures).
+
+Checks: every blob's dims re-derived by oracle/net.py from the reference's size rules; the
+Convolution layers of AlexNet / NiN / GoogLeNet at batch 1, 5, 20 are exactly the ops of the
+reference's own per-layer list conv-ops-1-5-20-nin-alex-gn.txt (which was generated from these
+nets); layer handling (Dropout / Data / Accuracy / Softmax dropped, in-place ReLU fused).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from boda_hip import ops
+from oracle import net as onet
+from oracle import oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "boda-1_amd", "bin", "boda_hip_rtc_fwd")
+NETS = os.path.join(ROOT, "tests", "golden", "nets")
+ALL = ["alexnet_ng_conv", "nin_imagenet", "googlenet_conv", "vgg_19", "resnet-50"]
+
+
+def plan(net, img):
+    r = subprocess.run([BIN, "--net", os.path.join(NETS, net + ".prototxt"), "--img", str(img), "--plan-json"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_det_hash_rand_restatement():
+    v = onet.det_hash_rand_vec(5000, 12345)
+    for i in list(range(0, 5000, 97)) + [4999]:
+        assert v[i] == np.float32(orc.det_hash_rand((i + 12345) & 0xFFFFFFFF))
+
+
+@pytest.mark.parametrize("net", ALL)
+def test_plan_dims(net):
+    p = plan(net, 20)
+    dims = onet.check_dims(p)
+    assert p["inputs"][0]["dims"][0] == 20
+    assert p["out_node"] in dims
+
+
+@pytest.mark.parametrize("net", ["alexnet_ng_conv", "nin_imagenet", "googlenet_conv"])
+def test_conv_layers_are_the_reference_op_list(net):
+    o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", "conv-ops-1-5-20-nin-alex-gn.txt"))
+    ref = {tuple(ops.shape_of(x).as_dims()) for x in o}
+    for img in (1, 5, 20):
+        p = plan(net, img)
+        dims = onet.check_dims(p)
+        for op in p["ops"]:
+            if op["type"] != "Convolution":
+                continue
+            B, C, H, W = dims[op["bots"][0]]
+            d = (B, C, H, W, op["out_chans"], op["k"][0], op["k"][1], op["s"][0], op["s"][1], op["p"][0], op["p"][1])
+            assert d in ref, (net, op["tag"], d)
+
+
+def test_layer_handling():
+    p = plan("alexnet_ng_conv", 1)
+    types = [o["type"] for o in p["ops"]]
+    assert "ReLU" not in types  # every ReLU runs in place on a conv output: fused
+    assert all(o["relu"] for o in p["ops"] if o["tag"] in ("conv1", "conv5", "fc6-conv"))
+    assert not [o for o in p["ops"] if o["tag"] == "fc8-conv"][0]["relu"]
+    ign = " ".join(p["ignored"])
+    assert "drop6" in ign and "accuracy" in ign and "Data layer" in ign
+    r = plan("resnet-50", 2)
+    t = {o["type"] for o in r["ops"]}
+    assert {"BatchNorm", "Scale", "Eltwise", "InnerProduct", "Pooling", "Convolution"} <= t
+    assert [o for o in r["ops"] if o["tag"] == "res2a"][0]["relu"]  # Eltwise + in-place ReLU fused
+    g = plan("googlenet_conv", 1)
+    cat = [o for o in g["ops"] if o["type"] == "Concat"]
+    assert len(cat) == 9 and all(len(o["bots"]) == 4 for o in cat)
+
+
+def test_bad_prototxt_reports_line(tmp_path):
+    f = tmp_path / "bad.prototxt"
+    f.write_text('name: "x"\nlayer {\n  name: "c"\n  type: "Convolution"\n  bottom: "data"\n')
+    r = subprocess.run([BIN, "--net", str(f), "--plan"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "prototxt line" in r.stderr

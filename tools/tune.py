@@ -31,7 +31,7 @@ from boda_hip import ops, runner  # noqa: E402
 
 SETS = {"sgemm-full": "sgemm-ops-full.txt", "sgemm-small": "sgemm-ops-small.txt",
         "conv": "conv-ops-1-5-20-nin-alex-gn.txt", "op-sigs": "op_sigs_full.txt"}
-SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
+SPLITS = [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 32, 48, 64]
 CFG_BK = {}
 
 
