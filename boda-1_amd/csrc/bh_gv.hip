@@ -269,6 +269,10 @@ std::vector<cfg_t> gv_cfgs() {
       gv_cfg<1, 1, 8, 4, 1>("gv16x16w8"),
       gv_cfg<1, 2, 8, 4, 1>("gv16x32w8"),
       gv_cfg<2, 1, 8, 4, 1>("gv32x16w8"),
+      // 16 waves: twice the loads in flight per CU for the smallest ops
+      gv_cfg<1, 1, 16, 2, 1>("gv16x16w16"),
+      gv_cfg<1, 2, 16, 2, 0>("gv16x32w16"),
+      gv_cfg<2, 1, 16, 2, 0>("gv32x16w16"),
   };
 }
 

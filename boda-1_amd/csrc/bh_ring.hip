@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
   // ---- per-lane DMA source state of the tile being issued, recomputed for every stage
   // without branches (a branch around it made hipcc drain the DMA ring, vmcnt(0), at the
   // K loop head; the recomputation is ~20 VALU + a few SALU per 32-deep K tile)
-  uint32_t a_lane = 0, b_lane = 0;
+  uint32_t a_lane = 0, b_lane = 0, ls_tile = 0xffffffffu;
   int col_base = 0, iy0 = 0, ix0 = 0;
   auto set_tile = [&](uint32_t t) {
     uint32_t tm, tn;
@@ -481,7 +481,10 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
   auto plan_stage = [&](uint32_t it, uint32_t(&vo)[LW]) {
     const bool live = it < it1;
     const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
-    set_tile(t);
+    if (t != ls_tile) {  // uniform: only at the issue side's tile changes
+      set_tile(t);
+      ls_tile = t;
+    }
     const uint32_t k0 = (it - t * p.ipt) * BK;
 #pragma unroll
     for (int j = 0; j < LA; ++j) vo[j] = a_lane + (k0 + RA * (wave * LA + j)) * p.lda * 4u;
