@@ -11,7 +11,11 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
-enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, B_IMTAB = 7, NBLD = 8 };
+enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, B_IMTAB = 7,
+       B_IMTAP = 8, NBLD = 9 };
+// B_IMTAP: ring kernels' im2col when IC % BK == 0: a K tile lies inside one filter tap, so a
+// stage has ONE per-lane tap offset (VGPR) and each k row adds a scalar channel offset through
+// the buffer instruction's soffset -- no per-row vector work
 // B_IMTAB: ring kernels' im2col for IC < BK (stem convs): the per-k-row (ic, ky, kx) decomposition
 // is tabulated in LDS once per block (TAB_MAX rows) instead of computed by scalar divisions
 // for every row of every stage
@@ -233,6 +237,9 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
+__device__ __forceinline__ void dma4s(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, voff, soff, 0, 0);
+}
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, voff, 0, 0, 0);
 }

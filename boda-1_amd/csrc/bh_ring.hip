@@ -29,7 +29,7 @@ template <int TM, int TN, int BK, int D, int BLD, int SPL>
 __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr int NW = 4, NT = 256;
   constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
-  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB);
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB || BLD == B_IMTAP);
   constexpr int TABF = BLD == B_IMTAB ? 2 * TAB_MAX : 0;  // im2col row table (int2 per k row)
   constexpr bool DW = IM || BLD == B_KSCALAR;  // B by dword DMA: one k row x 64 columns per instruction
   static_assert(BLD == B_KVEC || DW, "ring loaders: k-major 16-B or dword (SGEMM b), im2col / 1x1 dword");
@@ -112,7 +112,9 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
 
   // Per-lane source offsets of this wave's LW DMA instructions for the stage at k0 (A pieces
   // first, then B rows); computed up front so the DMA issues can be spread between MFMAs.
-  auto plan_stage = [&](uint32_t k0, uint32_t(&vo)[LW]) {
+  auto plan_stage = [&](uint32_t k0, uint32_t(&vo)[LW], uint32_t(&so)[LW]) {
+#pragma unroll
+    for (int q = 0; q < LW; ++q) so[q] = 0;
 #pragma unroll
     for (int j = 0; j < LA; ++j) vo[j] = a_lane + (k0 + RA * (wave * LA + j)) * p.lda * 4u;
     if constexpr (BLD == B_KVEC) {
@@ -144,6 +146,18 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
         vo[LA + j] = (nxt ? t1 : t0) + (nxt ? soff - ichw4 : soff);
         soff += RSTEP * hw4;
       }
+    } else if constexpr (BLD == B_IMTAP) {
+      // the stage's tap (scalar), its per-lane offset or a miss (one select for all rows),
+      // each row's channel offset as the scalar soffset
+      const uint32_t kyx = fdiv(k0, p.ic_m, p.ic_s);
+      const uint32_t ic0 = k0 - kyx * p.IC;
+      const uint32_t t0 = tap_off(kyx);
+      const uint32_t hw4 = p.HW * 4u;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        vo[LA + j] = t0;
+        so[LA + j] = (ic0 + rw0 + RSTEP * j) * hw4;
+      }
     } else if constexpr (BLD == B_IMTAB) {
       // tabulated rows: {ic*HW + ky*W + kx, ky | kx << 16} (rows past the range: ky = 0x7fff)
 #pragma unroll
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
     }
   };
   // DMA instruction q of this wave into ring slot `slot`
-  auto issue_one = [&](int q, int slot, uint32_t vo) {
+  auto issue_one = [&](int q, int slot, uint32_t vo, uint32_t so) {
     float *const Ab = smem + slot * SLOT;
     float *const Bb = Ab + A_LDS;
     if (q < LA) {
@@ -176,14 +190,15 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
     } else if constexpr (BLD == B_KVEC) {
       dma16(rsb, Bb + (wave * LB + q - LA) * 256, vo);
     } else {
-      dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
+      if constexpr (BLD == B_IMTAP) dma4s(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo, so);
+      else dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
     }
   };
   auto issue_stage = [&](int slot, uint32_t k0) {
-    uint32_t vo[LW];
-    plan_stage(k0, vo);
+    uint32_t vo[LW], so[LW];
+    plan_stage(k0, vo, so);
 #pragma unroll
-    for (int q = 0; q < LW; ++q) issue_one(q, slot, vo[q]);
+    for (int q = 0; q < LW; ++q) issue_one(q, slot, vo[q], so[q]);
   };
 
   f32x16 acc[TM][TN];
@@ -201,8 +216,8 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr int S2 = BK / 2;
   constexpr int PF = TM * TN >= 4 ? 1 : 2;  // LDS fragment prefetch distance (k steps)
   auto compute = [&](int slot, int islot, uint32_t k0) {
-    uint32_t vo[LW];
-    plan_stage(k0, vo);
+    uint32_t vo[LW], so[LW];
+    plan_stage(k0, vo, so);
     const float *const Ab = smem + slot * SLOT + kh * S2 * BM + wm * WM + TM * li;
     const float *const Bb = smem + slot * SLOT + A_LDS + kh * S2 * BN + wn * WN + TN * li;
     // fragments of step s+PF are read while step s's MFMAs run (a ds_read waited for right
@@ -229,7 +244,7 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
                                                            acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < LW; ++q)
-        if (q * S2 / LW == s) issue_one(q, islot, vo[q]);
+        if (q * S2 / LW == s) issue_one(q, islot, vo[q], so[q]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -764,6 +779,7 @@ cfg_t ring_conv_cfg(const char *name) {
   cfg_t c{name, 64 * TM, 64 * TN, BK, 256, {}, 1};
   reg_ring<TM, TN, BK, D, B_IM2COL>(c);
   reg_ring<TM, TN, BK, D, B_IMTAB>(c);
+  reg_ring<TM, TN, BK, D, B_IMTAP>(c);
   reg_ring<TM, TN, BK, D, B_IMT2>(c);
   reg_ring<TM, TN, BK, D, B_IM1X1>(c);
   return c;

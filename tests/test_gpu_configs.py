@@ -26,6 +26,7 @@ CONV_SHAPES = [
     ops.ConvShape(1, 520, 4, 4, 40, 1, 1, 1, 1, 0, 0),   # 1x1, long K (register ring wraps)
     ops.ConvShape(2, 70, 9, 7, 40, 3, 3, 1, 1, 1, 1),    # im2col, IC >= BK (ring: two-tap loader), ragged
     ops.ConvShape(1, 64, 12, 11, 96, 5, 5, 2, 2, 2, 2),  # im2col 5x5 stride 2, IC = 64
+    ops.ConvShape(2, 96, 13, 13, 100, 3, 3, 1, 1, 1, 1), # IC % BK == 0: one-tap K tiles (soffset loader), ragged M
 ]
 
 
