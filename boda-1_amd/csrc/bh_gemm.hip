@@ -955,6 +955,7 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
   p.tbn = c.BN;
   if (bld == B_IMTAB && !c.k[ald][bld][0]) bld = B_IM2COL;  // table / one-tap loaders: ring kernels only
   if (bld == B_IMTAP && !c.k[ald][bld][0]) bld = B_IMT2;
+  if (bld == B_IM1X1S && !c.k[ald][bld][0]) bld = B_IM1X1;
   if (c.gv) {
     // filter-streaming kernel (bh_gv.hip): one block per (64-row tile, K chunk); the K chunks
     // of a tile are combined by its last arriver. ch.splits = K chunks (0: ~1024 blocks)
@@ -1027,7 +1028,7 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
     const uint64_t total = nblk * c.BM * c.BN / 4;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
     const void *rk = (bld == B_IM2COL || bld == B_IMT2 || bld == B_IM1X1 || bld == B_IM1X1V || bld == B_IMTAB ||
-                      bld == B_IMTAP)
+                      bld == B_IMTAP || bld == B_IM1X1S)
                          ? (const void *)splitk_reduce_kernel<1>
                                                           : (const void *)splitk_reduce_kernel<0>;
     uint32_t Sv = S;
@@ -1178,7 +1179,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       set_fd(IC, p.ic_m, p.ic_s);
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
       const bool tab = ((p.K + bk - 1) / bk) * bk + 3 * bk <= (uint32_t)TAB_MAX;  // rows a block tabulates
-      const int bld = k1 ? B_IM1X1
+      const int bld = k1 ? (IC % bk == 0 ? B_IM1X1S : B_IM1X1)
                          : (IC >= bk ? (IC % bk == 0 ? B_IMTAP : B_IMT2) : (tab ? B_IMTAB : B_IM2COL));
       return launch_gemm(ctx, 1, ch, A_KVEC, bld, p, "conv", packed != nullptr);
     }

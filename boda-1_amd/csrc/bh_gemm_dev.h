@@ -12,7 +12,9 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
 enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, B_IMTAB = 7,
-       B_IMTAP = 8, NBLD = 9 };
+       B_IMTAP = 8, B_IM1X1S = 9, NBLD = 10 };
+// B_IM1X1S: ring kernels' 1x1 loader when K % BK == 0: the lane's pixel offset (VGPR, a miss
+// for dead stages) + each row's channel offset as the scalar soffset
 // B_IMTAP: ring kernels' im2col when IC % BK == 0: a K tile lies inside one filter tap, so a
 // stage has ONE per-lane tap offset (VGPR) and each k row adds a scalar channel offset through
 // the buffer instruction's soffset -- no per-row vector work

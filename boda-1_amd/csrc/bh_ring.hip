@@ -29,7 +29,9 @@ template <int TM, int TN, int BK, int D, int BLD, int SPL>
 __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr int NW = 4, NT = 256;
   constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
-  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB || BLD == B_IMTAP);
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB || BLD == B_IMTAP ||
+                       BLD == B_IM1X1S);
+  constexpr bool SOFF = (BLD == B_IMTAP || BLD == B_IM1X1S);  // rows differ by a scalar soffset only
   constexpr int TABF = BLD == B_IMTAB ? 2 * TAB_MAX : 0;  // im2col row table (int2 per k row)
   constexpr bool DW = IM || BLD == B_KSCALAR;  // B by dword DMA: one k row x 64 columns per instruction
   static_assert(BLD == B_KVEC || DW, "ring loaders: k-major 16-B or dword (SGEMM b), im2col / 1x1 dword");
@@ -91,7 +93,7 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
     const uint32_t col = bn0 + bgrp * 64 + (uint32_t)lane;
     const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
     const uint32_t pix = col - img * p.OHW;
-    if constexpr (BLD == B_IM1X1) {
+    if constexpr (BLD == B_IM1X1 || BLD == B_IM1X1S) {
       col_base = col < p.N ? (int)(img * p.ICHW + pix) * 4 : (int)OOB;
     } else {
       const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s);
@@ -146,6 +148,15 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
         vo[LA + j] = (nxt ? t1 : t0) + (nxt ? soff - ichw4 : soff);
         soff += RSTEP * hw4;
       }
+    } else if constexpr (BLD == B_IM1X1S) {
+      // K % BK == 0 and splits are whole K tiles: a stage is live (all rows valid) or dead
+      const uint32_t v = k0 < kend ? (uint32_t)col_base : OOB;
+      const uint32_t hw4 = p.HW * 4u;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        vo[LA + j] = v;
+        so[LA + j] = (k0 + rw0 + RSTEP * j) * hw4;
+      }
     } else if constexpr (BLD == B_IMTAP) {
       // the stage's tap (scalar), its per-lane offset or a miss (one select for all rows),
       // each row's channel offset as the scalar soffset
@@ -190,7 +201,7 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
     } else if constexpr (BLD == B_KVEC) {
       dma16(rsb, Bb + (wave * LB + q - LA) * 256, vo);
     } else {
-      if constexpr (BLD == B_IMTAP) dma4s(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo, so);
+      if constexpr (SOFF) dma4s(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo, so);
       else dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
     }
   };
@@ -780,6 +791,7 @@ cfg_t ring_conv_cfg(const char *name) {
   reg_ring<TM, TN, BK, D, B_IM2COL>(c);
   reg_ring<TM, TN, BK, D, B_IMTAB>(c);
   reg_ring<TM, TN, BK, D, B_IMTAP>(c);
+  reg_ring<TM, TN, BK, D, B_IM1X1S>(c);
   reg_ring<TM, TN, BK, D, B_IMT2>(c);
   reg_ring<TM, TN, BK, D, B_IM1X1>(c);
   return c;
@@ -834,6 +846,10 @@ std::vector<cfg_t> ring_cfgs(int op) {
       ring_conv_cfg<2, 1, 32, 3>("r128x64x32d3"),
       ring_conv_cfg<1, 2, 32, 3>("r64x128x32d3"),
       ring_conv_cfg<1, 4, 32, 2>("r64x256x32d2"),
+      // BK 16: IC % 16 == 0 shapes (144, 112, 48, 528 ...) take the one-tap loader
+      ring_conv_cfg<1, 2, 16, 4>("r64x128x16d4"),
+      ring_conv_cfg<2, 1, 16, 4>("r128x64x16d4"),
+      ring_conv_cfg<1, 1, 16, 4>("r64x64x16d4"),
       srk_conv_cfg<2, 2, 32, 2>("srk128x128x32d2"),
       srk_conv_cfg<2, 2, 16, 4>("srk128x128x16d4"),
       srk_conv_cfg<2, 2, 32, 4>("srk128x128x32d4"),

@@ -27,6 +27,8 @@ CONV_SHAPES = [
     ops.ConvShape(2, 70, 9, 7, 40, 3, 3, 1, 1, 1, 1),    # im2col, IC >= BK (ring: two-tap loader), ragged
     ops.ConvShape(1, 64, 12, 11, 96, 5, 5, 2, 2, 2, 2),  # im2col 5x5 stride 2, IC = 64
     ops.ConvShape(2, 96, 13, 13, 100, 3, 3, 1, 1, 1, 1), # IC % BK == 0: one-tap K tiles (soffset loader), ragged M
+    ops.ConvShape(2, 64, 9, 7, 70, 1, 1, 1, 1, 0, 0),    # 1x1, K % BK == 0 (soffset 1x1 loader), ragged N
+    ops.ConvShape(1, 256, 5, 5, 130, 1, 1, 1, 1, 0, 0),  # 1x1, K = 256 in several K tiles / splits
 ]
 
 
