@@ -985,9 +985,15 @@ int launch_gemm(bh_ctx *ctx, int op, choice_t const &ch, int ald, int bld, GemmA
     const uint32_t ipt = (p.K + c.BK - 1) / c.BK;
     const uint64_t total = nblk * ipt;
     if (total >= (1ull << 31)) return bh::fail(BH_UNSUP, std::string(what) + ": too many K iterations");
-    uint32_t bpc = ch.splits ? std::min<uint32_t>(ch.splits, 4) : std::max(1, std::min(2, 163840 / c.lds_bytes));
+    // splits 1..4: blocks per CU, iterations dealt equally (tiles cut between blocks);
+    // 5..8: blocks per CU 1..4, whole tiles per block (a persistent data-parallel grid whose
+    // DMA ring runs on across tiles: short-K ops, where cut tiles cost more than balance)
+    const bool whole = ch.splits > 4;
+    uint32_t bpc = ch.splits ? std::min<uint32_t>(whole ? ch.splits - 4 : ch.splits, 4)
+                             : std::max(1, std::min(2, 163840 / c.lds_bytes));
     uint64_t G = (uint64_t)ncu * bpc;
-    const uint32_t ipb = (uint32_t)((total + G - 1) / G);
+    uint32_t ipb = (uint32_t)((total + G - 1) / G);
+    if (whole) ipb = (uint32_t)((nblk + G - 1) / G) * ipt;
     G = (total + ipb - 1) / ipb;
     p.ipt = ipt;
     p.ipb = ipb;
@@ -1178,7 +1184,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       p.IC = IC;
       set_fd(IC, p.ic_m, p.ic_s);
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
-      const bool tab = ((p.K + bk - 1) / bk) * bk + 3 * bk <= (uint32_t)TAB_MAX;  // rows a block tabulates
+      const bool tab = ((p.K + bk - 1) / bk) * bk <= (uint32_t)TAB_MAX;  // K rows a block tabulates
       const int bld = k1 ? (IC % bk == 0 ? B_IM1X1S : B_IM1X1)
                          : (IC >= bk ? (IC % bk == 0 ? B_IMTAP : B_IMT2) : (tab ? B_IMTAB : B_IM2COL));
       return launch_gemm(ctx, 1, ch, A_KVEC, bld, p, "conv", packed != nullptr);

@@ -32,7 +32,8 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
   constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB || BLD == B_IMTAP ||
                        BLD == B_IM1X1S);
   constexpr bool SOFF = (BLD == B_IMTAP || BLD == B_IM1X1S);  // rows differ by a scalar soffset only
-  constexpr int TABF = BLD == B_IMTAB ? 2 * TAB_MAX : 0;  // im2col row table (int2 per k row)
+  // im2col row table (int2 per k row): up to TAB_MAX rows of K plus the D-1 dead stages past it
+  constexpr int TABF = BLD == B_IMTAB ? 2 * (TAB_MAX + (D - 1) * BK) : 0;
   constexpr bool DW = IM || BLD == B_KSCALAR;  // B by dword DMA: one k row x 64 columns per instruction
   static_assert(BLD == B_KVEC || DW, "ring loaders: k-major 16-B or dword (SGEMM b), im2col / 1x1 dword");
   static_assert(NW % TN == 0, "a wave's B columns: one 64-column group");
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
     }
   }
   if constexpr (BLD == B_IMTAB) {
-    // this block's K rows kbeg .. kbeg + (nkt + D - 1) * BK (the host checks <= TAB_MAX)
+    // this block's K rows kbeg .. kbeg + (nkt + D - 1) * BK (the host checks nkt * BK <= TAB_MAX)
     for (uint32_t r = tid; r < (nkt + D - 1) * BK; r += NT) {
       const uint32_t k = kbeg + r;
       const uint32_t kyx = k / p.IC, ic = k - kyx * p.IC;
@@ -438,7 +439,10 @@ template <int TM, int TN, int BK, int D, int BLD>
 __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
   constexpr int NW = 4, NT = 256;
   constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
-  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1);
+  constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAP || BLD == B_IM1X1S ||
+                       BLD == B_IMTAB);
+  constexpr int TABF = BLD == B_IMTAB ? 2 * TAB_MAX : 0;  // im2col row table of the op's K rows
+  constexpr bool SOFF = (BLD == B_IMTAP || BLD == B_IM1X1S);
   constexpr bool DW = IM;
   static_assert(BLD == B_KVEC || DW, "stream-K loaders: SGEMM 16-B, conv im2col / 1x1 dword");
   static_assert(NW % TN == 0, "a wave's B columns: one 64-column group");
@@ -452,8 +456,9 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
   constexpr int NCH = BM * BN / 4, CH = NCH / NT;  // float4 chunks of a tile, per thread
   static_assert(NCH % NT == 0, "combine chunking");
 
-  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + 4];
+  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + 4 + TABF];
   uint32_t *const flag = (uint32_t *)(smem + D * SLOT);
+  constexpr int TAB0 = D * SLOT + 4;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -486,7 +491,7 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
       const uint32_t col = bn0 + bgrp * 64 + (uint32_t)lane;
       const uint32_t img = fdiv(col, p.ohw_m, p.ohw_s);
       const uint32_t pix = col - img * p.OHW;
-      if constexpr (BLD == B_IM1X1) {
+      if constexpr (BLD == B_IM1X1 || BLD == B_IM1X1S) {
         col_base = col < p.N ? (int)(img * p.ICHW + pix) * 4 : (int)OOB;
       } else {
         const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s);
@@ -504,8 +509,10 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
     return oob_unless(ok, (uint32_t)(col_base + (int)(ky * p.W + kx)) * 4u);
   };
   // source offsets of this wave's LW DMA instructions for iteration `it` (all OOB past it1)
-  auto plan_stage = [&](uint32_t it, uint32_t(&vo)[LW]) {
+  auto plan_stage = [&](uint32_t it, uint32_t(&vo)[LW], uint32_t(&so)[LW]) {
     const bool live = it < it1;
+#pragma unroll
+    for (int q = 0; q < LW; ++q) so[q] = 0;
     const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
     if (t != ls_tile) {  // uniform: only at the issue side's tile changes
       set_tile(t);
@@ -522,6 +529,33 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
       for (int j = 0; j < LB; ++j) {
         const uint32_t k = k0 + rw0 + RSTEP * j;
         vo[LA + j] = (uint32_t)col_base + (k < p.K ? k * p.HW * 4u : 0x40000000u);
+      }
+    } else if constexpr (BLD == B_IM1X1S) {
+      const uint32_t hw4 = p.HW * 4u;  // K % BK == 0: every row of a live stage is valid
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        vo[LA + j] = (uint32_t)col_base;
+        so[LA + j] = (k0 + rw0 + RSTEP * j) * hw4;
+      }
+    } else if constexpr (BLD == B_IMTAP) {
+      const uint32_t kyx = fdiv(k0, p.ic_m, p.ic_s);  // IC % BK == 0: one tap per stage
+      const uint32_t ic0 = k0 - kyx * p.IC;
+      const uint32_t t0 = tap_off(kyx), hw4 = p.HW * 4u;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        vo[LA + j] = t0;
+        so[LA + j] = (ic0 + rw0 + RSTEP * j) * hw4;
+      }
+    } else if constexpr (BLD == B_IMTAB) {
+      // tabulated rows {ic*HW + ky*W + kx, ky | kx << 16} (float-typed reads, as in ring_kernel)
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const uint32_t r = k0 + rw0 + RSTEP * j;
+        const int ex = __builtin_bit_cast(int, smem[TAB0 + 2 * r]);
+        const int ey = __builtin_bit_cast(int, smem[TAB0 + 2 * r + 1]);
+        const int ky = ey & 0xffff, kx = ey >> 16;
+        const bool ok = ((uint32_t)(iy0 + ky) < p.H) & ((uint32_t)(ix0 + kx) < p.W);
+        vo[LA + j] = oob_unless(ok, (uint32_t)(col_base + ex) * 4u);
       }
     } else if constexpr (BLD == B_IMT2) {
       const uint32_t kf = k0 + rw0;
@@ -551,7 +585,7 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
 #pragma unroll
     for (int q = 0; q < LW; ++q) vo[q] |= dead;
   };
-  auto issue_one = [&](int q, int slot, uint32_t vo) {
+  auto issue_one = [&](int q, int slot, uint32_t vo, uint32_t so) {
     float *const Ab = smem + slot * SLOT;
     float *const Bb = Ab + A_LDS;
     if (q < LA) {
@@ -559,7 +593,8 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
     } else if constexpr (BLD == B_KVEC) {
       dma16(rsb, Bb + (wave * LB + q - LA) * 256, vo);
     } else {
-      dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
+      if constexpr (SOFF) dma4s(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo, so);
+      else dma4(rsb, Bb + (rw0 + RSTEP * (q - LA)) * BN + bgrp * 64, vo);
     }
   };
 
@@ -577,8 +612,8 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
   constexpr int S2 = BK / 2;
   constexpr int PF = TM * TN >= 4 ? 1 : 2;
   auto compute = [&](int slot, int islot, uint32_t it_issue) {
-    uint32_t vo[LW];
-    plan_stage(it_issue, vo);
+    uint32_t vo[LW], so[LW];
+    plan_stage(it_issue, vo, so);
     const float *const Ab = smem + slot * SLOT + kh * S2 * BM + wm * WM + TM * li;
     const float *const Bb = smem + slot * SLOT + A_LDS + kh * S2 * BN + wn * WN + TN * li;
     typename fvec<TM>::t av[PF + 1];
@@ -603,7 +638,7 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
                                                            acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < LW; ++q)
-        if (q * S2 / LW == s) issue_one(q, islot, vo[q]);
+        if (q * S2 / LW == s) issue_one(q, islot, vo[q], so[q]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -719,13 +754,24 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
     for (int j = 0; j < CH; ++j) finish_store<IM ? 1 : 0>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], nullptr);
   };
 
+  if constexpr (BLD == B_IMTAB) {
+    // the op's K rows 0 .. ipt * BK (the host checks <= TAB_MAX); rows past K: misses
+    for (uint32_t r = tid; r < p.ipt * BK; r += NT) {
+      const uint32_t kyx = r / p.IC, ic = r - kyx * p.IC;
+      const uint32_t ky = kyx / p.KX, kx = kyx - ky * p.KX;
+      const bool valid = r < p.K;
+      smem[TAB0 + 2 * r] = __builtin_bit_cast(float, valid ? (int)(ic * p.HW + ky * p.W + kx) : 0);
+      smem[TAB0 + 2 * r + 1] = __builtin_bit_cast(float, valid ? (int)(ky | (kx << 16)) : 0x7fff);
+    }
+    __syncthreads();
+  }
   // ---- main loop over this block's iterations: D-stage ring running across tiles
 #pragma unroll
   for (int s = 0; s < D - 1; ++s) {
-    uint32_t vo[LW];
-    plan_stage(it0 + s, vo);
+    uint32_t vo[LW], so[LW];
+    plan_stage(it0 + s, vo, so);
 #pragma unroll
-    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q], so[q]);
   }
   // outer loop over this block's tiles, inner loop over a tile's K iterations (a nested
   // loop keeps the accumulators in AGPRs: a flat loop with the tile epilogue inside made
@@ -802,6 +848,9 @@ cfg_t srk_conv_cfg(const char *name) {
   c.k[A_KVEC][B_IM2COL][0] = srk_kernel<TM, TN, BK, D, B_IM2COL>;
   c.k[A_KVEC][B_IMT2][0] = srk_kernel<TM, TN, BK, D, B_IMT2>;
   c.k[A_KVEC][B_IM1X1][0] = srk_kernel<TM, TN, BK, D, B_IM1X1>;
+  c.k[A_KVEC][B_IMTAP][0] = srk_kernel<TM, TN, BK, D, B_IMTAP>;
+  c.k[A_KVEC][B_IM1X1S][0] = srk_kernel<TM, TN, BK, D, B_IM1X1S>;
+  if constexpr (BK == 16 || TM * TN == 1) c.k[A_KVEC][B_IMTAB][0] = srk_kernel<TM, TN, BK, D, B_IMTAB>;
   return c;
 }
 template <int TM, int TN, int BK, int D>
@@ -850,6 +899,12 @@ std::vector<cfg_t> ring_cfgs(int op) {
       ring_conv_cfg<1, 2, 16, 4>("r64x128x16d4"),
       ring_conv_cfg<2, 1, 16, 4>("r128x64x16d4"),
       ring_conv_cfg<1, 1, 16, 4>("r64x64x16d4"),
+      // deeper rings: a short K (1x1, IC <= 80) fits the prologue, one memory round trip
+      ring_conv_cfg<1, 1, 16, 5>("r64x64x16d5"),
+      ring_conv_cfg<1, 1, 16, 7>("r64x64x16d7"),
+      ring_conv_cfg<1, 2, 16, 5>("r64x128x16d5"),
+      ring_conv_cfg<2, 1, 16, 5>("r128x64x16d5"),
+      ring_conv_cfg<1, 1, 32, 3>("r64x64x32d3"),
       srk_conv_cfg<2, 2, 32, 2>("srk128x128x32d2"),
       srk_conv_cfg<2, 2, 16, 4>("srk128x128x16d4"),
       srk_conv_cfg<2, 2, 32, 4>("srk128x128x32d4"),
@@ -859,6 +914,8 @@ std::vector<cfg_t> ring_cfgs(int op) {
       srk_conv_cfg<1, 2, 32, 4>("srk64x128x32d4"),
       srk_conv_cfg<1, 2, 32, 3>("srk64x128x32d3"),
       srk_conv_cfg<1, 1, 32, 4>("srk64x64x32d4"),
+      srk_conv_cfg<1, 1, 16, 4>("srk64x64x16d4"),
+      srk_conv_cfg<1, 2, 16, 4>("srk64x128x16d4"),
       srk_conv_cfg<1, 4, 32, 3>("srk64x256x32d3"),
   };
 }

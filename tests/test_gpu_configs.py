@@ -91,11 +91,13 @@ SRK_CONV_SHAPES = [
     ops.ConvShape(16, 64, 64, 64, 100, 1, 1, 1, 1, 0, 0),  # 1x1, K = 64: several whole tiles per block
     ops.ConvShape(2, 64, 30, 30, 96, 3, 3, 1, 1, 1, 1),    # two-tap loader, every tile cut
     ops.ConvShape(2, 3, 50, 50, 64, 7, 7, 2, 2, 3, 3),     # IC < BK stem conv, stride 2
+    ops.ConvShape(2, 48, 20, 20, 96, 3, 3, 1, 1, 1, 1),    # BK 32: two-tap loader; BK 16: one-tap
+    ops.ConvShape(4, 40, 20, 20, 70, 1, 1, 1, 1, 0, 0),    # 1x1, K % BK != 0: per-row loader
 ]
 
 
 @pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("srk")])
-@pytest.mark.parametrize("bpc", [1, 2])
+@pytest.mark.parametrize("bpc", [1, 2, 5, 6])
 def test_conv_streamk(dev, cn, bpc):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), bpc)
     try:
@@ -112,7 +114,7 @@ def test_conv_streamk(dev, cn, bpc):
 
 
 @pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(0) if n.startswith("srk")])
-@pytest.mark.parametrize("bpc", [1, 2])
+@pytest.mark.parametrize("bpc", [1, 2, 6])
 def test_sgemm_streamk(dev, cn, bpc):
     dev.tune_set(0, boda_hip.tune_cfg_names(0).index(cn), bpc)
     try:

@@ -95,6 +95,10 @@ def main():
     ap.add_argument("--timing", choices=["graph", "flush"], default="graph")
     ap.add_argument("--max-flop-sgemm", type=float, default=3e12, help="skip sgemm sweeps above this (use heuristic)")
     ap.add_argument("--merge", action="store_true", help="keep --out entries of ops not swept in this run")
+    ap.add_argument("--min-gain", type=float, default=0.03, help="with --cfg-re: replace the table's choice "
+                    "only if the new best is this much faster (timings vary a few %% from box to box)")
+    ap.add_argument("--cfg-re", default="", help="sweep only configs matching this regex (plus the --out "
+                    "table's current choice for the op, timed again, so the better one is kept)")
     args = ap.parse_args()
     global TIMING
     TIMING = args.timing
@@ -103,6 +107,12 @@ def main():
     plat = dev.plat_tag()
     names = {0: boda_hip.tune_cfg_names(0), 1: boda_hip.tune_cfg_names(1)}
     table, results = {}, []
+    prev = {}
+    if args.cfg_re and os.path.exists(args.out):
+        for l in open(args.out):
+            m = re.match(r"(.*) cfg=(\S+) splits=(\d+) red=(\w)", l)
+            if m:
+                prev[m.group(1)] = (m.group(2), int(m.group(3)) * (-1 if m.group(4) == "k" else 1))
     t_start = time.time()
     for sname in args.sets.split(","):
         o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", SETS[sname]))
@@ -125,9 +135,11 @@ def main():
             cand = []
             if not (kind == 0 and s.flops() > args.max_flop_sgemm):
                 for ci, cn in enumerate(names[kind]):
+                    if args.cfg_re and not re.search(args.cfg_re, cn):
+                        continue
                     nkt = -(-K // bk_of(cn))
                     if cn.startswith("srk"):  # stream-K: S = blocks per CU
-                        cand += [(ci, 1), (ci, 2)]
+                        cand += [(ci, 1), (ci, 2), (ci, 5), (ci, 6)]  # 5, 6: whole tiles per block
                         continue
                     if cn.startswith("gv"):  # register-streaming kernels: S = K chunks
                         tiles = -(-M // int(cn[2:].split("x")[0])) * -(-N // int(cn.split("x")[1].split("w")[0]))
@@ -140,6 +152,8 @@ def main():
                         cand.append((ci, S))
                         if S > 1:
                             cand.append((ci, -S))  # same split, separate reduce kernel
+            if key in prev and prev[key][0] in names[kind]:
+                cand.append((names[kind].index(prev[key][0]), prev[key][1]))
             for ci, S in cand:
                 dev.tune_set(kind, ci, S)
                 try:
@@ -152,6 +166,11 @@ def main():
             dev.tune_set(kind, -1, 0)
             wl.free()
             results.append({"key": key, "cfg": "default", "splits": 0, "ms": t_def})
+            if key in prev:  # keep the table's choice unless clearly beaten in this run
+                pt = [x["ms"] for x in results if x["key"] == key and x["cfg"] == prev[key][0]
+                      and x["splits"] == prev[key][1]]
+                if pt and best[0] >= (1 - args.min_gain) * pt[0]:
+                    best = (pt[0], names[kind].index(prev[key][0]), prev[key][1])
             if best[1] >= 0:
                 table[key] = (names[kind][best[1]], best[2], best[0], t_def)
             rf = runner.roofline_secs(s) * 1e3
