@@ -1126,11 +1126,15 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases, float *out, uint32_t B,
                 uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
-                uint32_t sx, uint32_t py, uint32_t px, int relu) {
+                uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot) {
+  // out_ctot: channels of the tensor `out` points into (0: OC). Every conv epilogue addresses
+  // image i of the output at i * OCOHW, so a conv can write its channel slab of a wider
+  // tensor (a Concat's output) in place.
+  if (!out_ctot) out_ctot = OC;
   const uint32_t OH = (H + 2 * py - KY) / sy + 1, OW = (W + 2 * px - KX) / sx + 1;
   const uint64_t K = (uint64_t)IC * KY * KX, P = (uint64_t)B * OH * OW;
   const uint64_t in_bytes = (uint64_t)B * IC * H * W * 4, w_bytes = (uint64_t)OC * K * 4;
-  if (!fits_buffer(in_bytes) || !fits_buffer(w_bytes) || !fits_buffer((uint64_t)B * OC * OH * OW * 4))
+  if (!fits_buffer(in_bytes) || !fits_buffer(w_bytes) || !fits_buffer((uint64_t)B * out_ctot * OH * OW * 4))
     return fail(BH_UNSUP, "conv: tensor larger than 2 GiB");
   if (K >= (1u << 31) || P >= (1u << 31)) return fail(BH_UNSUP, "conv: GEMM extent too large");
   GemmArgs p{};
@@ -1143,7 +1147,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   p.cvec = (OH * OW) % 4 == 0 && ((uintptr_t)out % 16 == 0);  // output rows take float4 stores
   p.H = H; p.W = W; p.KX = KX; p.KYX = KY * KX;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px;
-  p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = OC * OH * OW;
+  p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = out_ctot * OH * OW;
   set_fd(p.KYX, p.kyx_m, p.kyx_s);
   set_fd(KX, p.kx_m, p.kx_s);
   set_fd(p.OHW, p.ohw_m, p.ohw_s);

@@ -2,6 +2,8 @@
 // executor over rtc_compute_t (be=hip). See conv_pipe.H for the reference map.
 #include "conv_pipe.H"
 
+#include <algorithm>
+
 #include <cmath>
 #include <cstring>
 #include <set>
@@ -412,6 +414,95 @@ namespace {
 dims_t vec_dims(std::string const &n, uint32_t sz) { return dims_t({{n, sz}}); }
 }  // namespace
 
+// Inference BatchNorm (mean, var, eps) or Scale (gamma, beta) as out = in * sc[c] + sh[c];
+// synthetic statistics: mean ~ U(-0.1, 0.1), var ~ U(0.5, 1.5), gamma ~ 1 + U(-0.1, 0.1)
+void affine_params(conv_op_t const &op, uint32_t C, std::vector<float> &sc, std::vector<float> &sh) {
+  sc.assign(C, 0.0f);
+  sh.assign(C, 0.0f);
+  std::vector<float> a(C), b(C);
+  if (op.type == "BatchNorm") {
+    synth_param(a, param_seed(op.tag, "mean"), 0.1f / 5.0f);
+    synth_param(b, param_seed(op.tag, "var"), 0.5f / 5.0f);
+    for (uint32_t c = 0; c < C; ++c) {
+      const float var = 1.0f + b[c];
+      sc[c] = 1.0f / std::sqrt(var + op.k);
+      sh[c] = -a[c] * sc[c];
+    }
+  } else {
+    synth_param(a, param_seed(op.tag, "gamma"), 0.1f / 5.0f);
+    synth_param(b, param_seed(op.tag, "beta"), 0.1f / 5.0f);
+    for (uint32_t c = 0; c < C; ++c) {
+      sc[c] = 1.0f + a[c];
+      sh[c] = op.bias_term ? b[c] : 0.0f;
+    }
+  }
+}
+
+// Inference-time folding: a BatchNorm / Scale running in place on the output of the
+// Convolution / InnerProduct just before it (and of nothing else: no ReLU in between) is a
+// per-output-channel affine of that conv's result, so it is folded into the conv's bank and
+// biases at init (w' = w * s, b' = b * s + t): one kernel and one HBM round trip of the
+// activation less per affine (resnet-50: 106 of its 230 layer calls). A ReLU fused into the
+// last folded affine moves to the conv.
+void conv_pipe_fwd_t::plan_folds() {
+  folds.clear();
+  folded.clear();
+  conv_op_t const *tgt = nullptr;
+  for (auto const &p : cp->ops) {
+    conv_op_t const &op = *p;
+    if ((op.type == "Convolution" || op.type == "InnerProduct") && op.tops.size() == 1) {
+      tgt = op.fused_relu ? nullptr : &op;
+    } else if ((op.type == "BatchNorm" || op.type == "Scale") && tgt && !op.fused && op.bots.size() == 1 &&
+               op.tops == op.bots && op.bots[0] == tgt->tops[0]) {
+      folds[tgt->tag].push_back(&op);
+      folded.insert(op.tag);
+      if (op.fused_relu) tgt = nullptr;
+    } else {
+      tgt = nullptr;
+    }
+  }
+}
+
+std::string conv_pipe_fwd_t::exec_plan_str() const {
+  std::ostringstream o;
+  for (auto const &kv : folds)
+    for (conv_op_t const *a : kv.second) o << "fold " << a->type << " " << a->tag << " -> " << kv.first << "\n";
+  for (auto const &kv : slabs) o << "slab " << kv.first << " -> " << kv.second.first << " @" << kv.second.second << "\n";
+  return o.str();
+}
+
+// Concat in place: a Concat input produced by a Convolution / InnerProduct (out of place) and
+// read by nothing but that Concat is written by the conv straight into its channel slab of the
+// Concat's output (bh_conv2d_fwd_nchw_slab); the Concat then copies only its other inputs.
+// The reference copies every input (src/rtc_fwd.cc:267-280). googlenet: 36 of its 36 Concat
+// inputs, one activation write + read less each.
+void conv_pipe_fwd_t::plan_slabs() {
+  slabs.clear();
+  std::map<std::string, conv_op_t const *> producer;
+  std::map<std::string, uint32_t> readers;  // ops that run and read the blob
+  for (auto const &p : cp->ops) {
+    conv_op_t const &op = *p;
+    if (op.fused || folded.count(op.tag)) continue;
+    for (auto const &b : op.bots) ++readers[b];
+    for (auto const &t : op.tops) producer[t] = &op;
+  }
+  for (auto const &p : cp->ops) {
+    conv_op_t const &op = *p;
+    if (op.type != "Concat" || op.fused) continue;
+    uint32_t oc0 = 0;
+    for (auto const &b : op.bots) {
+      auto pr = producer.find(b);
+      const uint32_t nc = cp->node_dims.at(b).dsz("chan");
+      const bool conv = pr != producer.end() && (pr->second->type == "Convolution" || pr->second->type == "InnerProduct");
+      const bool src = std::find(cp->inputs.begin(), cp->inputs.end(), b) != cp->inputs.end();
+      if (conv && !src && readers[b] == 1 && b != cp->out_node && pr->second->bots[0] != b &&
+          std::count(op.bots.begin(), op.bots.end(), b) == 1)
+        slabs[b] = {op.tops[0], oc0};
+      oc0 += nc;
+    }
+  }
+}
+
 void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
   if (op.fused) return;
   dims_t const &in = cp->node_dims.at(op.bots[0]);
@@ -446,18 +537,38 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     rtc->create_var_with_dims(fv, fo.dims_vals["filts"]);
     std::vector<float> w((size_t)s.OC * s.IC * s.KY * s.KX);
     synth_param(w, param_seed(op.tag, "filts"), std::sqrt(3.0f / (float)(s.IC * s.KY * s.KX)) / 5.0f);
+    std::vector<float> b(s.OC, 0.0f);
+    if (op.bias_term) synth_param(b, param_seed(op.tag, "biases"), 0.1f / 5.0f);
+    auto fit = folds.find(op.tag);
+    const bool fold = fit != folds.end();
+    if (fold) {
+      const size_t kk = (size_t)s.IC * s.KY * s.KX;
+      std::vector<float> sc, sh;
+      for (conv_op_t const *a : fit->second) {
+        affine_params(*a, s.OC, sc, sh);
+        for (uint32_t oc = 0; oc < s.OC; ++oc) {
+          for (size_t k = 0; k < kk; ++k) w[oc * kk + k] *= sc[oc];
+          b[oc] = b[oc] * sc[oc] + sh[oc];
+        }
+        if (a->fused_relu) fo.scalars["conv_has_relu"] = 1;
+      }
+    }
     upload(fv, w);
-    bool bias = op.bias_term;
+    const bool bias = op.bias_term || fold;
     if (bias) {
       rtc->create_var_with_dims(bv, fo.dims_vals["biases"]);
-      std::vector<float> b(s.OC);
-      synth_param(b, param_seed(op.tag, "biases"), 0.1f / 5.0f);
       upload(bv, b);
     }
-    ensure_out(op.tops[0]);
+    std::string ov = op.tops[0];
+    auto sl = slabs.find(ov);
+    if (sl != slabs.end()) {  // write the channel slab of the Concat's output
+      ov = sl->second.first;
+      fo.scalars["out_chan_ofs"] = sl->second.second;
+    }
+    ensure_out(ov);
     std::string fn = "hip_conv__" + op.tag;
     rtc->compile({{fn, "", {}, fo}}, rtc_compile_opts_t());
-    std::map<std::string, rtc_arg_t> args{{"in", op.bots[0]}, {"filts", fv}, {"out", op.tops[0]}};
+    std::map<std::string, rtc_arg_t> args{{"in", op.bots[0]}, {"filts", fv}, {"out", ov}};
     if (bias) args["biases"] = bv;
     if (pack_filts && !ip) {
       // Boda's xpose_filts at init (src/rtc_fwd.cc:306-326): the k-major bank the ring kernels read
@@ -511,6 +622,10 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     uint32_t oc0 = 0;
     for (size_t i = 0; i < op.bots.size(); ++i) {
       const uint32_t nc = cp->node_dims.at(op.bots[i]).dsz("chan");
+      if (slabs.count(op.bots[i])) {  // its producer wrote the slab already
+        oc0 += nc;
+        continue;
+      }
       op_base_t f2 = fo;
       f2.scalars = {{"ic0", 0}, {"oc0", oc0}, {"nc", nc}};
       std::string fn = "hip_copy__" + op.tag + "_" + std::to_string(i);
@@ -521,26 +636,9 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     return;
   }
   if (op.type == "BatchNorm" || op.type == "Scale") {
-    // inference BatchNorm (mean, var, eps) and Scale (gamma, beta) as one per-channel affine;
-    // synthetic statistics: mean ~ U(-0.1, 0.1), var ~ U(0.5, 1.5), gamma ~ 1 + U(-0.1, 0.1)
-    std::vector<float> sc(C), sh(C);
-    std::vector<float> a(C), b(C);
-    if (op.type == "BatchNorm") {
-      synth_param(a, param_seed(op.tag, "mean"), 0.1f / 5.0f);
-      synth_param(b, param_seed(op.tag, "var"), 0.5f / 5.0f);
-      for (uint32_t c = 0; c < C; ++c) {
-        const float var = 1.0f + b[c];
-        sc[c] = 1.0f / std::sqrt(var + op.k);
-        sh[c] = -a[c] * sc[c];
-      }
-    } else {
-      synth_param(a, param_seed(op.tag, "gamma"), 0.1f / 5.0f);
-      synth_param(b, param_seed(op.tag, "beta"), 0.1f / 5.0f);
-      for (uint32_t c = 0; c < C; ++c) {
-        sc[c] = 1.0f + a[c];
-        sh[c] = op.bias_term ? b[c] : 0.0f;
-      }
-    }
+    if (folded.count(op.tag)) return;  // folded into the producing Convolution's bank and biases
+    std::vector<float> sc, sh;
+    affine_params(op, C, sc, sh);
     std::string sv = op.tag + "_scale", tv = op.tag + "_shift";
     rtc->create_var_with_dims(sv, vec_dims("chan", C));
     rtc->create_var_with_dims(tv, vec_dims("chan", C));
@@ -579,6 +677,8 @@ void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, p_rtc_compute_t const &rtc_
     rtc->create_var_with_dims(in, cp->node_dims.at(in));
     declared.insert(in);
   }
+  if (fold_affines) plan_folds();
+  if (concat_in_place) plan_slabs();
   for (auto const &op : cp->ops) gen_op(*op);
   rtc->finish_and_sync();
 }
@@ -598,6 +698,10 @@ void conv_pipe_fwd_t::run_fwd(std::map<std::string, p_nda_t> const &inputs) {
     t.flops = calls[i].flops;
     times.push_back(t);
   }
+}
+
+double conv_pipe_fwd_t::time_fwd_graph(uint32_t reps) {
+  return rtc->time_graph([&] { for (auto const &c : calls) rtc->run(c.rfc); }, reps);
 }
 
 double conv_pipe_fwd_t::sum_ms() const {

@@ -51,6 +51,7 @@ struct hip_compute_t : public rtc_compute_t {
   bh_ctx *ctx = nullptr;
   std::map<std::string, var_info_t> vars;
   std::map<std::string, rtc_func_info_t> funcs;
+  bool capturing = false;  // inside time_graph's capture
   std::vector<call_ev_t> calls;
 
   explicit hip_compute_t(int dev) : device(dev) {}
@@ -144,8 +145,9 @@ struct hip_compute_t : public rtc_compute_t {
     if (fit == funcs.end()) rt_err("hip_compute: function '" + rfc.rtc_func_name + "' not compiled");
     rtc_func_info_t const &fi = fit->second;
     call_ev_t ev{};
-    // events on the call's own first/last kernel dispatch (no host launch latency)
-    bh_check(bh_time_next_call(ctx, &ev.b, &ev.e), "bh_time_next_call");
+    // events on the call's own first/last kernel dispatch (no host launch latency); none while
+    // capturing a graph (time_graph times the replays)
+    if (!capturing) bh_check(bh_time_next_call(ctx, &ev.b, &ev.e), "bh_time_next_call");
     std::string const &fn = fi.func_name;
     const std::string kind = kind_of(fn);
     auto sc = [&](char const *n) -> uint32_t {
@@ -218,10 +220,21 @@ struct hip_compute_t : public rtc_compute_t {
       auto r = fi.op.scalars.find("conv_has_relu");
       int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
       // filts_xp (optional): the bank hip_xpose_filts made before the timed calls
-      bh_check(bh_conv2d_fwd_nchw_pk(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
-                                     arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
-                                     s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
-               "hip_conv");
+      auto oc0 = fi.op.scalars.find("out_chan_ofs");
+      if (oc0 == fi.op.scalars.end()) {
+        bh_check(bh_conv2d_fwd_nchw_pk(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
+                                       arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
+                                       s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
+                 "hip_conv");
+      } else {  // a channel slab of a wider output (a Concat's, written in place)
+        uint32_t OB, OCT, OH, OW;
+        nchw("out", OB, OCT, OH, OW);
+        if (OB != s.B || OH != s.OH || OW != s.OW) rt_err(fn + ": out dims do not match the conv");
+        bh_check(bh_conv2d_fwd_nchw_slab(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
+                                         arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), OCT, (uint32_t)oc0->second,
+                                         s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
+                 "hip_conv");
+      }
     } else if (kind == "hip_xpose_filts") {  // Boda's xpose_filts (test/rtc/xpose_filts.cucl) for hip_conv
       conv_shape_t s = get_conv_shape(fi.op);
       if (arg_dims(rfc, "filts_xp").elems() != bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX))
@@ -259,6 +272,33 @@ struct hip_compute_t : public rtc_compute_t {
     float ms = 0;
     bh_check(bh_elapsed_ms(ctx, calls[b].b, calls[e].e, &ms), "bh_elapsed_ms");
     return ms;
+  }
+  double time_graph(std::function<void()> const &issue, uint32_t reps) override {
+    if (!reps) rt_err("time_graph: reps == 0");
+    bh_check(bh_sync(ctx), "bh_sync");
+    bh_check(bh_capture_begin(ctx), "bh_capture_begin");
+    int g = -1;
+    capturing = true;
+    try {
+      issue();
+    } catch (...) {
+      capturing = false;
+      (void)bh_capture_end(ctx, &g);
+      if (g >= 0) (void)bh_graph_destroy(ctx, g);
+      throw;
+    }
+    capturing = false;
+    bh_check(bh_capture_end(ctx, &g), "bh_capture_end");
+    bh_check(bh_graph_launch(ctx, g), "bh_graph_launch");  // warm: graph upload, caches
+    bh_check(bh_sync(ctx), "bh_sync");
+    int b = -1, e = -1;
+    bh_check(bh_event_record(ctx, &b), "bh_event_record");
+    for (uint32_t r = 0; r < reps; ++r) bh_check(bh_graph_launch(ctx, g), "bh_graph_launch");
+    bh_check(bh_event_record(ctx, &e), "bh_event_record");
+    float ms = 0;
+    bh_check(bh_elapsed_ms(ctx, b, e, &ms), "bh_elapsed_ms");
+    bh_check(bh_graph_destroy(ctx, g), "bh_graph_destroy");
+    return ms / reps;
   }
   void profile_start() override {}
   void profile_stop() override {}

@@ -4,9 +4,15 @@
 // gen_data mode 5 (det_hash_rand(i + 234234567), the reference's Convolution `in` seed).
 //
 //   boda_hip_rtc_fwd --net nets/alexnet/train_val.prototxt [--img 20] [--out-node pool5]
-//                    [--iters 5] [--plan | --plan-json] [--save DIR] [--device 0] [--no-pack]
+//                    [--iters 5] [--plan | --plan-json] [--save DIR] [--device 0] [--no-pack] [--no-fold]
 //
-// --plan / --plan-json print the net plan without touching a GPU (host logic tests);
+// --plan / --plan-json print the net plan without touching a GPU (host logic tests); --plan-exec
+// the executor's BatchNorm/Scale folds and in-place Concat slabs;
+// --no-fold runs BatchNorm / Scale as separate affine layers instead of folding them into the
+// producing conv (conv_pipe_fwd_t::plan_folds); --no-inplace-concat copies every Concat input
+// instead of letting its producing conv write the Concat's channel slab (plan_slabs).
+// --graph R also times the whole forward captured as one hipGraph, replayed R times (ms per
+// forward with every launch seam; the per-layer list is event-timed per call).
 // --save writes DIR/in.f32 and DIR/out.f32 (raw little-endian fp32) for the parity tests.
 #include <cmath>
 #include <cstdio>
@@ -80,7 +86,8 @@ int main(int argc, char **argv) {
   std::string net, out_node, save;
   uint32_t img = 0, iters = 3;
   int device = 0;
-  bool plan = false, plan_js = false, pack = true;
+  bool plan = false, plan_js = false, plan_exec = false, pack = true, fold = true, inplace = true;
+  uint32_t graph_reps = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -98,7 +105,11 @@ int main(int argc, char **argv) {
     else if (a == "--save") save = val();
     else if (a == "--plan") plan = true;
     else if (a == "--plan-json") plan_js = true;
+    else if (a == "--plan-exec") plan_exec = true;
     else if (a == "--no-pack") pack = false;
+    else if (a == "--no-fold") fold = false;
+    else if (a == "--graph") graph_reps = (uint32_t)atoi(val().c_str());
+    else if (a == "--no-inplace-concat") inplace = false;
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
@@ -106,11 +117,19 @@ int main(int argc, char **argv) {
   }
   if (net.empty()) {
     fprintf(stderr, "usage: boda_hip_rtc_fwd --net <prototxt> [--img N] [--out-node n] [--iters K] "
-                    "[--plan|--plan-json] [--save DIR] [--device d] [--no-pack]\n");
+                    "[--plan|--plan-json|--plan-exec] [--save DIR] [--device d] [--no-pack] [--no-fold] [--no-inplace-concat] [--graph R]\n");
     return 2;
   }
   try {
     p_conv_pipe_t cp = create_pipe_from_prototxt(read_file(net), img, out_node);
+    if (plan_exec) {  // the executor's folds / in-place Concat slabs (no GPU)
+      conv_pipe_fwd_t fwd;
+      fwd.cp = cp;
+      if (fold) fwd.plan_folds();
+      if (inplace) fwd.plan_slabs();
+      printf("%s", fwd.exec_plan_str().c_str());
+      return 0;
+    }
     if (plan || plan_js) {
       if (plan_js) printf("%s\n", plan_json(*cp).c_str());
       else {
@@ -124,6 +143,8 @@ int main(int argc, char **argv) {
     rtc->init();
     conv_pipe_fwd_t fwd;
     fwd.pack_filts = pack;
+    fwd.fold_affines = fold;
+    fwd.concat_in_place = inplace;
     fwd.init(cp, rtc);
     auto in = std::make_shared<nda_t>(cp->node_dims.at(cp->inputs[0]));
     for (uint64_t i = 0; i < in->dims.elems(); ++i) in->elems()[i] = det_hash_rand((uint32_t)i + 234234567u);
@@ -137,11 +158,18 @@ int main(int argc, char **argv) {
     printf("net %s  plat %s  input %s  out %s %s\n", cp->name.c_str(), rtc->get_plat_tag().c_str(),
            cp->node_dims.at(cp->inputs[0]).str().c_str(), cp->out_node.c_str(),
            cp->node_dims.at(cp->out_node).str().c_str());
-    for (auto const &t : fwd.times)
-      printf("  %-28s %-34s %9.4f ms %s\n", t.tag.c_str(), t.func.c_str(), t.ms,
-             t.flops > 0 ? (std::to_string((int)(t.flops / t.ms / 1e6)) + " GFLOP/s").c_str() : "");
+    for (auto const &t : fwd.times) {
+      char rate[32] = "";
+      if (t.flops > 0 && t.ms > 0) snprintf(rate, sizeof(rate), "%.1f GFLOP/s", t.flops / t.ms / 1e6);
+      printf("  %-28s %-34s %9.4f ms %s\n", t.tag.c_str(), t.func.c_str(), t.ms, rate);
+    }
     printf("total (best of %u) %.4f ms  conv GFLOP %.3f  %.1f GFLOP/s\n", std::max(1u, iters), best, flops / 1e9,
            flops / best / 1e6);
+    if (graph_reps) {
+      const double g = fwd.time_fwd_graph(graph_reps);
+      printf("forward as one hipGraph (%zu calls, %u replays) %.4f ms  %.1f GFLOP/s\n", fwd.times.size(), graph_reps, g,
+             flops / g / 1e6);
+    }
     if (!save.empty()) {
       write_f32(save + "/in.f32", *in);
       write_f32(save + "/out.f32", *fwd.get(cp->out_node));

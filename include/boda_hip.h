@@ -156,6 +156,16 @@ int bh_conv2d_fwd_nchw_pk(bh_ctx *ctx, const float *in, const float *filts, cons
                           const float *biases, float *out, uint32_t B, uint32_t IC, uint32_t H,
                           uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
                           uint32_t sx, uint32_t py, uint32_t px, int relu);
+/* bh_conv2d_fwd_nchw_pk writing channels out_chan_ofs .. out_chan_ofs+OC-1 of an output
+ * tensor B x out_chans_total x OH x OW (out points at its start): a conv whose only reader is
+ * a Concat writes its slab of the Concat's output in place, so the net executor runs no
+ * channel copy for it (the reference's conv_pipe_fwd_t copies every Concat input with
+ * copy.cucl, src/rtc_fwd.cc:267-280). */
+int bh_conv2d_fwd_nchw_slab(bh_ctx *ctx, const float *in, const float *filts, const float *packed,
+                            const float *biases, float *out, uint32_t out_chans_total,
+                            uint32_t out_chan_ofs, uint32_t B, uint32_t IC, uint32_t H, uint32_t W,
+                            uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx,
+                            uint32_t py, uint32_t px, int relu);
 
 /* ---- the other forward layers of Boda's net executor (conv_pipe_fwd_t::gen_op,
  *      src/rtc_fwd.cc:263-405), NCHW fp32 ------------------------------------ */

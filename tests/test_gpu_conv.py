@@ -139,3 +139,37 @@ def test_unsupported_is_reported(dev):
     s = ops.ConvShape(1, 1, 2, 2, 1, 5, 5, 1, 1, 0, 0)  # kernel larger than padded input
     with pytest.raises(boda_hip.UnsupportedError):
         run_conv(dev, s)
+
+
+SLAB_SHAPES = [
+    ops.ConvShape(20, 480, 14, 14, 64, 1, 1, 1, 1, 0, 0),  # 1x1, latency / ring kernels
+    ops.ConvShape(20, 192, 28, 28, 128, 3, 3, 1, 1, 1, 1),  # 3x3 ring kernel
+    ops.ConvShape(1, 832, 7, 7, 48, 1, 1, 1, 1, 0, 0),  # register-streaming kernel, OH*OW % 4 != 0
+    ops.ConvShape(5, 160, 7, 7, 320, 3, 3, 1, 1, 1, 1),  # K-split combine
+    ops.ConvShape(5, 32, 28, 28, 96, 5, 5, 1, 1, 2, 2),
+    ops.ConvShape(2, 3, 35, 35, 16, 7, 7, 2, 2, 3, 3),  # stem (IC < BK)
+]
+
+
+@pytest.mark.parametrize("s", SLAB_SHAPES, ids=lambda s: "x".join(map(str, s.as_dims())))
+def test_conv_writes_channel_slab(dev, s):
+    """bh_conv2d_fwd_nchw_slab (a conv writing its channels of a Concat's output in place):
+    the slab holds exactly the bits of the plain call, every other channel is untouched."""
+    ref = run_conv(dev, s).reshape(s.B, s.OC, s.OH, s.OW)
+    ofs, ctot = 16, s.OC + 40
+    i = dev.alloc_floats(s.B * s.IC * s.H * s.W)
+    f = dev.alloc_floats(s.OC * s.K)
+    b = dev.alloc_floats(s.OC)
+    o = dev.alloc_floats(s.B * ctot * s.OH * s.OW)
+    dev.gen_data(GEN_CONV_IN, i, [s.B, s.IC, s.H, s.W], 5)
+    dev.gen_data(GEN_CONV_FILTS, f, [s.OC, s.IC, s.KY, s.KX], 5)
+    dev.gen_data(GEN_CONV_BIASES, b, [s.OC], 5)
+    o.upload(np.full(s.B * ctot * s.OH * s.OW, -7.25, np.float32))
+    dev.conv_slab(i, f, b, o, ctot, ofs, s)
+    got = o.download().reshape(s.B, ctot, s.OH, s.OW)
+    with pytest.raises(boda_hip.BodaHipError):  # slab past the tensor's channels
+        dev.conv_slab(i, f, b, o, ctot, ctot - s.OC + 1, s)
+    for x in (i, f, b, o):
+        x.free()
+    np.testing.assert_array_equal(got[:, ofs:ofs + s.OC], ref)
+    assert (got[:, :ofs] == -7.25).all() and (got[:, ofs + s.OC:] == -7.25).all()

@@ -60,3 +60,29 @@ def test_net_unpacked_bank_same_bits(tmp_path):
     _, _, g1, _ = run_net("alexnet_ng_conv", 2, a)
     _, _, g2, _ = run_net("alexnet_ng_conv", 2, b, ["--no-pack"])
     np.testing.assert_array_equal(g1, g2)
+
+
+def test_resnet_bn_scale_folded(tmp_path):
+    """BatchNorm / Scale folded into the producing conv (conv_pipe_fwd_t::plan_folds): no
+    affine kernel runs, and the output matches the unfolded executor to fp32 rounding."""
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _, _, g1, log1 = run_net("resnet-50", 1, a)
+    _, _, g2, log2 = run_net("resnet-50", 1, b, ["--no-fold"])
+    assert "hip_affine__" not in log1 and log2.count("hip_affine__") == 106
+    nm, rl2, _ = orc.normalized_errors(g2, g1)
+    assert rl2 <= 1e-5 and nm <= 1e-4, (nm, rl2)
+
+
+def test_googlenet_concat_in_place_same_bits(tmp_path):
+    """Convs writing their Concat slab in place (plan_slabs) give the copying executor's bits."""
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _, _, g1, log1 = run_net("googlenet_conv", 2, a)
+    _, _, g2, log2 = run_net("googlenet_conv", 2, b, ["--no-inplace-concat"])
+    np.testing.assert_array_equal(g1, g2)
+    assert log1.count("hip_copy__") < log2.count("hip_copy__")

@@ -82,3 +82,24 @@ def test_bad_prototxt_reports_line(tmp_path):
     f.write_text('name: "x"\nlayer {\n  name: "c"\n  type: "Convolution"\n  bottom: "data"\n')
     r = subprocess.run([BIN, "--net", str(f), "--plan"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "prototxt line" in r.stderr
+
+
+def exec_plan(net, *extra):
+    r = subprocess.run([BIN, "--net", os.path.join(NETS, net + ".prototxt"), "--plan-exec"] + list(extra),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.splitlines()
+
+
+def test_exec_plan_folds_and_slabs():
+    """The executor's rewrites (conv_pipe_fwd_t::plan_folds / plan_slabs), planned on the host."""
+    r = exec_plan("resnet-50")
+    assert len(r) == 106 and all(l.startswith("fold ") for l in r)  # every BatchNorm and Scale
+    assert "fold BatchNorm bn_conv1 -> conv1" in r and "fold Scale scale_conv1 -> conv1" in r
+    assert exec_plan("resnet-50", "--no-fold") == []
+    g = exec_plan("googlenet_conv")
+    assert len(g) == 36 and all(l.startswith("slab ") for l in g)  # 9 Concats x 4 conv inputs
+    assert "slab icp1_out1 -> icp2_in @64" in g
+    assert exec_plan("googlenet_conv", "--no-inplace-concat") == []
+    for n in ("alexnet_ng_conv", "nin_imagenet", "vgg_19"):
+        assert exec_plan(n) == []
