@@ -48,38 +48,56 @@ __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in,
 // LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): one thread per (img, y, x), a
 // running sum of squares over a window of LS channels kept with a ring of the last LS inputs
 // (+ new^2 - old^2, the reference's order), out = in * (k + alpha/LS * sum)^-beta.
+// The thread's channel walk is a serial dependency chain, so the inputs are fetched in groups
+// of G channels with the next group's loads in flight while the current one is summed (G
+// loads per thread outstanding instead of LS), and blocks are one wave so the few threads an
+// LRN has (B*H*W: 14580 for AlexNet norm2 at batch 20) spread over 4x more CUs.
 template <int LS>
-__global__ __launch_bounds__(256) void lrn_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                  float *__restrict__ out_scale_base, uint32_t npix, uint32_t C,
-                                                  uint32_t HW, float alpha, float beta, float k) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void lrn_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                 float *__restrict__ out_scale_base, uint32_t npix, uint32_t C,
+                                                 uint32_t HW, float alpha, float beta, float k) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   if (i >= npix) return;
   const uint32_t img = i / HW, pix = i - img * HW;
   const size_t base = (size_t)img * C * HW + pix;
   constexpr int hls = LS >> 1;
+  constexpr int G = LS * (LS >= 32 ? 1 : 32 / LS);  // channels per group; a multiple of LS (static ring slots)
   const float alpha_over_ls = alpha / (float)LS;
   float ring[LS];
 #pragma unroll
   for (int j = 0; j < LS; ++j) ring[j] = 0.0f;
+  float cur[G], nxt[G];
+  auto load = [&](int c0, float (&v)[G]) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int c = c0 + j;
+      v[j] = c < (int)C ? in[base + (size_t)c * HW] : 0.0f;
+    }
+  };
   float sum = 0.0f;
   const int n = (int)C + hls;
-  for (int c0 = 0; c0 < n; c0 += LS) {
+  load(0, cur);
+  for (int c0 = 0; c0 < n; c0 += G) {
+    if (c0 + G < n) load(c0 + G, nxt);
 #pragma unroll
-    for (int j = 0; j < LS; ++j) {  // channel c = c0 + j sits in ring slot j (c % LS)
+    for (int j = 0; j < G; ++j) {  // channel c = c0 + j sits in ring slot j % LS (c % LS)
       const int c = c0 + j;
       if (c < n) {
-        const float old = ring[j];
-        ring[j] = c < (int)C ? in[base + (size_t)c * HW] : 0.0f;
-        sum += ring[j] * ring[j];
+        const int r = j % LS;
+        const float old = ring[r];
+        ring[r] = cur[j];
+        sum += ring[r] * ring[r];
         sum -= old * old;
         if (c >= hls) {
           const int oc = c - hls;
           const float sb = k + sum * alpha_over_ls;
           if (out_scale_base) out_scale_base[base + (size_t)oc * HW] = sb;
-          out[base + (size_t)oc * HW] = ring[(j + LS - hls) % LS] * powf(sb, -beta);
+          out[base + (size_t)oc * HW] = ring[(r + LS - hls) % LS] * powf(sb, -beta);
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < G; ++j) cur[j] = nxt[j];
   }
 }
 
@@ -219,7 +237,7 @@ int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, 
     case 11: kern = (const void *)lrn_kernel<11>; break;
     default: return fail(BH_UNSUP, "lrn: local_size must be odd and <= 11");
   }
-  return launch(ctx, kern, dim3((npix + 255) / 256), dim3(256), args, true, true, "lrn");
+  return launch(ctx, kern, dim3((npix + 63) / 64), dim3(64), args, true, true, "lrn");
 }
 
 int launch_relu(bh_ctx *ctx, float *x, uint64_t n) {

@@ -86,3 +86,18 @@ def test_googlenet_concat_in_place_same_bits(tmp_path):
     _, _, g2, log2 = run_net("googlenet_conv", 2, b, ["--no-inplace-concat"])
     np.testing.assert_array_equal(g1, g2)
     assert log1.count("hip_copy__") < log2.count("hip_copy__")
+
+
+@pytest.mark.parametrize("net", ["googlenet_conv", "resnet-50"])
+def test_forward_graph_replay(net, tmp_path):
+    """The whole forward captured as one hipGraph and replayed (--graph): it runs, reports a
+    time, and leaves the eager forward's output bits."""
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _, _, g1, _ = run_net(net, 2, a)
+    _, _, g2, log = run_net(net, 2, b, ["--graph", "3"])
+    np.testing.assert_array_equal(g1, g2)
+    line = [l for l in log.splitlines() if l.startswith("forward as one hipGraph")]
+    assert len(line) == 1 and float(line[0].split(")")[1].split()[0]) > 0, log
