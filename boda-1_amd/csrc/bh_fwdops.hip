@@ -13,91 +13,96 @@ namespace {
 // count, for max and for average (the average divides by the number of in-image taps).
 // out_in_yx (may be null): for max pooling, the in_y*W + in_x of the winning input (-1 if
 // none), stored as a float as the reference does.
+// KY_/KX_ > 0: the window is a compile-time constant (3x3 and 2x2: every pooling layer of
+// the reference nets but the global ones), so the loop unrolls and all taps' loads issue
+// together instead of one guarded load per loop trip.
+template <int KY_, int KX_>
 __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                    float *__restrict__ out_in_yx, uint32_t total, uint32_t C,
-                                                   uint32_t H, uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY,
-                                                   uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
-                                                   int avg) {
+                                                   uint32_t H, uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY_rt,
+                                                   uint32_t KX_rt, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
+                                                   int avg, uint32_t ow_m, uint32_t ow_s, uint32_t oh_m, uint32_t oh_s) {
+  const uint32_t KY = KY_ > 0 ? (uint32_t)KY_ : KY_rt, KX = KX_ > 0 ? (uint32_t)KX_ : KX_rt;
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  const uint32_t ox = i % OW, t = i / OW, oy = t % OH, nc = t / OH;  // nc = img * C + chan
+  // i -> (nc, oy, ox) with multiply-shift division (nc = img * C + chan)
+  const uint32_t t = (__umulhi(i, ow_m) + i) >> ow_s, ox = i - t * OW;
+  const uint32_t nc = (__umulhi(t, oh_m) + t) >> oh_s, oy = t - nc * OH;
   const float *const src = in + (size_t)nc * H * W;
   float v = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
   int oyx = -1;
-  // the reference's loop order (kx outer, ky inner) decides ties and the summation order
-  for (uint32_t kx = 0; kx < KX; ++kx)
-    for (uint32_t ky = 0; ky < KY; ++ky) {
-      const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
-      if (iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H) {
-        const float x = src[iy * W + ix];
-        if (avg) {
-          v += x;
-          cnt += 1.0f;
-        } else if (x > v) {
-          v = x;
-          oyx = iy * (int)W + ix;
-        }
+  // the reference's loop order (kx outer, ky inner) decides ties and the summation order; a
+  // tap in the padding loads src[0] (always valid) and is then ignored, so no load is guarded
+  auto tap = [&](uint32_t ky, uint32_t kx) {
+    const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
+    const bool ok = iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H;
+    const float x = src[ok ? iy * (int)W + ix : 0];
+    if (ok) {
+      if (avg) {
+        v += x;
+        cnt += 1.0f;
+      } else if (x > v) {
+        v = x;
+        oyx = iy * (int)W + ix;
       }
     }
+  };
+  if constexpr (KY_ > 0 && KX_ > 0) {
+#pragma unroll
+    for (int kx = 0; kx < KX_; ++kx)
+#pragma unroll
+      for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
+  } else {
+    for (uint32_t kx = 0; kx < KX; ++kx)
+      for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
+  }
   if (avg) v /= cnt;
   out[i] = v;
   if (out_in_yx) out_in_yx[i] = (float)oyx;
   (void)C;
 }
 
-// LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): one thread per (img, y, x), a
-// running sum of squares over a window of LS channels kept with a ring of the last LS inputs
-// (+ new^2 - old^2, the reference's order), out = in * (k + alpha/LS * sum)^-beta.
-// The thread's channel walk is a serial dependency chain, so the inputs are fetched in groups
-// of G channels with the next group's loads in flight while the current one is summed (G
-// loads per thread outstanding instead of LS), and blocks are one wave so the few threads an
-// LRN has (B*H*W: 14580 for AlexNet norm2 at batch 20) spread over 4x more CUs.
+// LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): a running sum of squares over a
+// window of LS channels kept with a ring of the last LS inputs (+ new^2 - old^2, the
+// reference's order), out = in * (k + alpha/LS * sum)^-beta.
+// The reference gives each (img, y, x) one thread walking all C channels: a serial chain of C
+// powf's and loads on only B*H*W threads (14580 for AlexNet norm2 at batch 20, < 1 wave per
+// SIMD). Here a thread owns LRN_CH output channels of one pixel (threads of a wave: adjacent
+// pixels, coalesced): it loads its LRN_CH + LS - 1 inputs up front and runs the same ring
+// from channel c0 - LS/2 (zeros before channel 0, as the reference's ring starts). The first
+// chunk is the reference's sequence exactly; later chunks start their running sum fresh (the
+// window sum without the earlier channels' +/- residue: within 1 ulp-scale of it).
+constexpr int LRN_CH = 16;
 template <int LS>
-__global__ __launch_bounds__(64) void lrn_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                 float *__restrict__ out_scale_base, uint32_t npix, uint32_t C,
-                                                 uint32_t HW, float alpha, float beta, float k) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= npix) return;
+__global__ __launch_bounds__(256) void lrn_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                  float *__restrict__ out_scale_base, uint32_t npix, uint32_t C,
+                                                  uint32_t HW, float alpha, float beta, float k, uint32_t total) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const uint32_t chunk = t / npix, i = t - chunk * npix;
   const uint32_t img = i / HW, pix = i - img * HW;
   const size_t base = (size_t)img * C * HW + pix;
-  constexpr int hls = LS >> 1;
-  constexpr int G = LS * (LS >= 32 ? 1 : 32 / LS);  // channels per group; a multiple of LS (static ring slots)
+  constexpr int hls = LS >> 1, NI = LRN_CH + 2 * hls;
+  const int c0 = (int)chunk * LRN_CH;  // first output channel
   const float alpha_over_ls = alpha / (float)LS;
-  float ring[LS];
+  float x[NI];  // inputs c0 - hls .. c0 + LRN_CH + hls - 1
 #pragma unroll
-  for (int j = 0; j < LS; ++j) ring[j] = 0.0f;
-  float cur[G], nxt[G];
-  auto load = [&](int c0, float (&v)[G]) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const int c = c0 + j;
-      v[j] = c < (int)C ? in[base + (size_t)c * HW] : 0.0f;
-    }
-  };
+  for (int j = 0; j < NI; ++j) {
+    const int c = c0 - hls + j;
+    x[j] = (c >= 0 && c < (int)C) ? in[base + (size_t)c * HW] : 0.0f;
+  }
   float sum = 0.0f;
-  const int n = (int)C + hls;
-  load(0, cur);
-  for (int c0 = 0; c0 < n; c0 += G) {
-    if (c0 + G < n) load(c0 + G, nxt);
 #pragma unroll
-    for (int j = 0; j < G; ++j) {  // channel c = c0 + j sits in ring slot j % LS (c % LS)
-      const int c = c0 + j;
-      if (c < n) {
-        const int r = j % LS;
-        const float old = ring[r];
-        ring[r] = cur[j];
-        sum += ring[r] * ring[r];
-        sum -= old * old;
-        if (c >= hls) {
-          const int oc = c - hls;
-          const float sb = k + sum * alpha_over_ls;
-          if (out_scale_base) out_scale_base[base + (size_t)oc * HW] = sb;
-          out[base + (size_t)oc * HW] = ring[(r + LS - hls) % LS] * powf(sb, -beta);
-        }
-      }
+  for (int j = 0; j < NI; ++j) {
+    const float old = j >= LS ? x[j - LS] : 0.0f;  // the ring slot's previous occupant
+    sum += x[j] * x[j];
+    sum -= old * old;
+    const int oc = c0 - hls + j - hls;
+    if (j >= 2 * hls && oc < (int)C) {
+      const float sb = k + sum * alpha_over_ls;
+      if (out_scale_base) out_scale_base[base + (size_t)oc * HW] = sb;
+      out[base + (size_t)oc * HW] = x[j - hls] * powf(sb, -beta);
     }
-#pragma unroll
-    for (int j = 0; j < G; ++j) cur[j] = nxt[j];
   }
 }
 
@@ -217,16 +222,23 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
   const uint64_t total = (uint64_t)B * C * OH * OW;
   if (total >= (1ull << 31) || (uint64_t)B * C * H * W >= (1ull << 31)) return fail(BH_UNSUP, "pool: tensor too large");
   uint32_t tot = (uint32_t)total;
-  void *args[] = {&in, &out, &out_in_yx, &tot, &C, &H, &W, (void *)&OH, (void *)&OW, &KY, &KX, &sy, &sx, &py, &px, &avg};
-  return launch(ctx, (const void *)pool_kernel, dim3((tot + 255) / 256), dim3(256), args, true, true, "pool");
+  const fastdiv fow = make_fastdiv(OW), foh = make_fastdiv(OH);
+  uint32_t ow_m = fow.m, ow_s = fow.s, oh_m = foh.m, oh_s = foh.s;
+  void *args[] = {&in,  &out, &out_in_yx, &tot, &C,   &H,   &W,   (void *)&OH, (void *)&OW, &KY,
+                  &KX,  &sy,  &sx,        &py,  &px,  &avg, &ow_m, &ow_s,      &oh_m,       &oh_s};
+  const void *kern = KY == 3 && KX == 3   ? (const void *)pool_kernel<3, 3>
+                     : KY == 2 && KX == 2 ? (const void *)pool_kernel<2, 2>
+                                          : (const void *)pool_kernel<0, 0>;
+  return launch(ctx, kern, dim3((tot + 255) / 256), dim3(256), args, true, true, "pool");
 }
 
 int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
                uint32_t W, uint32_t local_size, float alpha, float beta, float k) {
   const uint64_t np = (uint64_t)B * H * W;
   if (np * C >= (1ull << 31)) return fail(BH_UNSUP, "lrn: tensor too large");
-  uint32_t npix = (uint32_t)np, HW = H * W;
-  void *args[] = {&in, &out, &out_scale_base, &npix, &C, &HW, &alpha, &beta, &k};
+  const uint64_t tot64 = np * ((C + LRN_CH - 1) / LRN_CH);  // threads: pixels x channel chunks
+  uint32_t npix = (uint32_t)np, HW = H * W, total = (uint32_t)tot64;
+  void *args[] = {&in, &out, &out_scale_base, &npix, &C, &HW, &alpha, &beta, &k, &total};
   const void *kern = nullptr;
   switch (local_size) {
     case 1: kern = (const void *)lrn_kernel<1>; break;
@@ -237,7 +249,7 @@ int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, 
     case 11: kern = (const void *)lrn_kernel<11>; break;
     default: return fail(BH_UNSUP, "lrn: local_size must be odd and <= 11");
   }
-  return launch(ctx, kern, dim3((npix + 63) / 64), dim3(64), args, true, true, "lrn");
+  return launch(ctx, kern, dim3((total + 255) / 256), dim3(256), args, true, true, "lrn");
 }
 
 int launch_relu(bh_ctx *ctx, float *x, uint64_t n) {
