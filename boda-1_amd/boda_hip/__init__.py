@@ -28,7 +28,7 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
            "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
            "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
-           "bh_eltwise", "bh_conv2d_fwd_nchw_slab"]
+           "bh_eltwise", "bh_conv2d_fwd_nchw_slab", "bh_conv2d_fwd_nchw_res"]
 
 
 class BodaHipError(RuntimeError):
@@ -73,6 +73,7 @@ def lib():
         L.bh_sgemm_kmajor.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32]
         L.bh_conv2d_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
         L.bh_conv2d_fwd_nchw_pk.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 11 + [ctypes.c_int]
+        L.bh_conv2d_fwd_nchw_res.argtypes = [c_vp] * 7 + [c_u32] * 11 + [ctypes.c_int]
         L.bh_conv2d_fwd_nchw_slab.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 13 + [ctypes.c_int]
         L.bh_conv_filts_packed_floats.argtypes = [c_u32] * 4
         L.bh_conv_filts_packed_floats.restype = ctypes.c_size_t
@@ -275,6 +276,12 @@ class Device:
         else:
             _check(lib().bh_conv2d_fwd_nchw_pk(self.ctx, inp.ptr, filts.ptr, packed.ptr, bp, out.ptr, s.B, s.IC, s.H,
                                                s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu)))
+
+    def conv_res(self, inp, filts, biases, res, out, s, relu=1, packed=None):
+        """bh_conv2d_fwd_nchw_res: out = relu(conv + bias + res)."""
+        _check(lib().bh_conv2d_fwd_nchw_res(self.ctx, inp.ptr, filts.ptr, packed.ptr if packed is not None else None,
+                                            biases.ptr if biases is not None else None, res.ptr, out.ptr, s.B, s.IC,
+                                            s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu)))
 
     def conv_slab(self, inp, filts, biases, out, out_chans_total, out_chan_ofs, s, relu=1, packed=None):
         """bh_conv2d_fwd_nchw_slab: channels out_chan_ofs .. +OC of a B x out_chans_total x OH x OW output."""

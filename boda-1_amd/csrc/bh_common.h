@@ -78,7 +78,8 @@ int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], u
 int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t M, uint32_t N, uint32_t K);
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
                 float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
-                uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0);
+                uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0,
+                const float *res = nullptr);
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX);

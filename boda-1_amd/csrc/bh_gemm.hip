@@ -343,7 +343,10 @@ __global__ __launch_bounds__(WAVES_M *WAVES_N * 64) void gemm_kernel(GemmArgs p)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         float x = acc[i][j][r];
-        if constexpr (IM) x += Lbias[wm * WM + TM * row + i];
+        if constexpr (IM) {
+          x += Lbias[wm * WM + TM * row + i];
+          if (p.res && cofs[j] >= 0) x += p.res[(size_t)m * p.OHW + cofs[j]];  // residual (Eltwise SUM)
+        }
         v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
       }
       if constexpr (IM) {
@@ -1126,7 +1129,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases, float *out, uint32_t B,
                 uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
-                uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot) {
+                uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot, const float *res) {
   // out_ctot: channels of the tensor `out` points into (0: OC). Every conv epilogue addresses
   // image i of the output at i * OCOHW, so a conv can write its channel slab of a wider
   // tensor (a Concat's output) in place.
@@ -1138,13 +1141,14 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     return fail(BH_UNSUP, "conv: tensor larger than 2 GiB");
   if (K >= (1u << 31) || P >= (1u << 31)) return fail(BH_UNSUP, "conv: GEMM extent too large");
   GemmArgs p{};
-  p.a = filts; p.b = in; p.c = out; p.bias = biases;
+  p.a = filts; p.b = in; p.c = out; p.bias = biases; p.res = res;
   p.M = OC; p.N = (uint32_t)P; p.K = (uint32_t)K;
   p.lda = (uint32_t)K; p.ldb = 0; p.ldc = 0;
   p.a_bytes = (uint32_t)w_bytes;
   p.b_bytes = (uint32_t)in_bytes;
   p.relu = relu;
-  p.cvec = (OH * OW) % 4 == 0 && ((uintptr_t)out % 16 == 0);  // output rows take float4 stores
+  p.cvec = (OH * OW) % 4 == 0 && ((uintptr_t)out % 16 == 0) &&
+           ((uintptr_t)res % 16 == 0);  // output (and residual) rows take float4 accesses
   p.H = H; p.W = W; p.KX = KX; p.KYX = KY * KX;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px;
   p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = out_ctot * OH * OW;

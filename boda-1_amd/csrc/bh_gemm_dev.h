@@ -47,6 +47,7 @@ struct GemmArgs {
   uint32_t tiles_m, tiles_n;
   int relu;
   int cvec;  // dense C rows can take TN-wide vector stores
+  const float *res;  // conv only, may be null: out = relu(conv + bias + res), res laid out like out
   // implicit im2col (B_IM2COL / B_IM1X1); N = B*OH*OW, K = IC*KY*KX
   uint32_t H, W, KX, KYX, sy, sx, py, px, OW, OHW, HW, ICHW, OCOHW;
   uint32_t kyx_m, kyx_s, kx_m, kx_s, ohw_m, ohw_s, ow_m, ow_s;  // fastdiv constants
@@ -132,18 +133,18 @@ __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_
   if (m >= p.M) return;
   const uint32_t n0 = tile_n * p.tbn + col0;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float x = sum[t] + b;
-    sum[t] = (p.relu && x < 0.0f) ? 0.0f : x;
-  }
+  for (int t = 0; t < 4; ++t) sum[t] += b;
   if (p.cvec && n0 + 4 <= p.N) {
     size_t o;
     if constexpr (IMODE) {
       const uint32_t img = fdiv(n0, p.ohw_m, p.ohw_s);
       o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n0 - img * p.OHW);
+      if (p.res) sum += *(const f32x4v *)&p.res[o];
     } else {
       o = (size_t)m * p.ldc + n0;
     }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) sum[t] = (p.relu && sum[t] < 0.0f) ? 0.0f : sum[t];
     *(f32x4v *)&p.c[o] = sum;
     return;
   }
@@ -151,11 +152,14 @@ __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_
   for (int t = 0; t < 4; ++t) {
     const uint32_t n = n0 + t;
     if (n >= p.N) break;
+    float x = sum[t];
     if constexpr (IMODE) {
       const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
-      p.c[(size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW)] = sum[t];
+      const size_t o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW);
+      if (p.res) x += p.res[o];
+      p.c[o] = (p.relu && x < 0.0f) ? 0.0f : x;
     } else {
-      p.c[(size_t)m * p.ldc + n] = sum[t];
+      p.c[(size_t)m * p.ldc + n] = (p.relu && x < 0.0f) ? 0.0f : x;
     }
   }
 }

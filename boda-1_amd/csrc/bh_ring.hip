@@ -378,7 +378,10 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         float x = acc[i][j][r];
-        if constexpr (IM) x += Lbias[wm * WM + TM * row + i];
+        if constexpr (IM) {
+          x += Lbias[wm * WM + TM * row + i];
+          if (p.res && cofs[j] >= 0) x += p.res[(size_t)m * p.OHW + cofs[j]];  // residual (Eltwise SUM)
+        }
         v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
       }
       if constexpr (IM) {
@@ -671,7 +674,9 @@ __global__ __launch_bounds__(256) void srk_kernel(GemmArgs p) {
           float v[TN];
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            const float x = acc[i][j][r] + bias;
+            float x = acc[i][j][r] + bias;
+            if constexpr (IM)
+              if (p.res && cofs[j] >= 0) x += p.res[(size_t)m * p.OHW + cofs[j]];  // residual (Eltwise SUM)
             v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
           }
           if constexpr (IM) {

@@ -247,6 +247,17 @@ int bh_conv2d_fwd_nchw_pk(bh_ctx *c, const float *in, const float *filts, const 
   return bh::launch_conv(c, in, filts, packed, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu);
 }
 
+int bh_conv2d_fwd_nchw_res(bh_ctx *c, const float *in, const float *filts, const float *packed, const float *biases,
+                           const float *res, float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC,
+                           uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
+  BH_CHECK_CTX(c);
+  if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
+    return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
+  if (H + 2 * py < KY || W + 2 * px < KX) return bh::fail(BH_UNSUP, "conv: padded input smaller than kernel");
+  return bh::launch_conv(c, in, filts, packed, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, 0, res);
+}
+
 int bh_conv2d_fwd_nchw_slab(bh_ctx *c, const float *in, const float *filts, const float *packed,
                             const float *biases, float *out, uint32_t out_chans_total, uint32_t out_chan_ofs,
                             uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,

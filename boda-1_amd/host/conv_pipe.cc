@@ -463,8 +463,49 @@ void conv_pipe_fwd_t::plan_folds() {
   }
 }
 
+bool conv_pipe_fwd_t::conv_relu(conv_op_t const &conv) const {
+  auto f = folds.find(conv.tag);
+  return conv.fused_relu || (f != folds.end() && !f->second.empty() && f->second.back()->fused_relu);
+}
+
+// Residual add in the conv epilogue: an Eltwise SUM of two blobs, one of them written by the
+// Convolution that runs just before it (no ReLU of its own, read by nothing else), becomes
+// that conv's epilogue out = relu?(conv + bias + other) (bh_conv2d_fwd_nchw_res; the same
+// adds in the same order, so bit-identical). ResNet-50: its 16 shortcut sums, one activation
+// write + two reads less each.
+void conv_pipe_fwd_t::plan_resadds() {
+  resadds.clear();
+  res_fused.clear();
+  std::map<std::string, uint32_t> readers;
+  for (auto const &p : cp->ops) {
+    if (p->fused || folded.count(p->tag)) continue;
+    for (auto const &b : p->bots) ++readers[b];
+  }
+  conv_op_t const *prev = nullptr;
+  for (auto const &p : cp->ops) {
+    conv_op_t const &op = *p;
+    if (op.fused || folded.count(op.tag)) continue;
+    if (op.type == "Eltwise" && op.eltwise_op == "SUM" && op.bots.size() == 2 && op.tops.size() == 1 && prev &&
+        prev->type == "Convolution" && prev->tops.size() == 1 && !conv_relu(*prev)) {
+      std::string const &cv = prev->tops[0];
+      const int w = op.bots[0] == cv ? 0 : (op.bots[1] == cv ? 1 : -1);
+      if (w >= 0) {
+        std::string const &other = op.bots[1 - w];
+        if (other != cv && readers[cv] == 1 && op.tops[0] != other && cv != cp->out_node &&
+            cp->node_dims.at(other) == cp->node_dims.at(cv) && cp->node_dims.at(op.tops[0]) == cp->node_dims.at(cv)) {
+          resadds[prev->tag] = {op.tag, op.tops[0], other, op.fused_relu};
+          res_fused.insert(op.tag);
+        }
+      }
+    }
+    prev = &op;
+  }
+}
+
 std::string conv_pipe_fwd_t::exec_plan_str() const {
   std::ostringstream o;
+  for (auto const &kv : resadds)
+    o << "resadd " << kv.second.eltwise << " -> " << kv.first << (kv.second.relu ? " +relu" : "") << "\n";
   for (auto const &kv : folds)
     for (conv_op_t const *a : kv.second) o << "fold " << a->type << " " << a->tag << " -> " << kv.first << "\n";
   for (auto const &kv : slabs) o << "slab " << kv.first << " -> " << kv.second.first << " @" << kv.second.second << "\n";
@@ -482,7 +523,7 @@ void conv_pipe_fwd_t::plan_slabs() {
   std::map<std::string, uint32_t> readers;  // ops that run and read the blob
   for (auto const &p : cp->ops) {
     conv_op_t const &op = *p;
-    if (op.fused || folded.count(op.tag)) continue;
+    if (op.fused || folded.count(op.tag) || res_fused.count(op.tag)) continue;
     for (auto const &b : op.bots) ++readers[b];
     for (auto const &t : op.tops) producer[t] = &op;
   }
@@ -565,11 +606,17 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
       ov = sl->second.first;
       fo.scalars["out_chan_ofs"] = sl->second.second;
     }
+    auto ra = resadds.find(op.tag);
+    if (ra != resadds.end()) {  // the Eltwise SUM (+ ReLU) after this conv, in its epilogue
+      ov = ra->second.out;
+      fo.scalars["conv_has_relu"] = ra->second.relu ? 1 : 0;
+    }
     ensure_out(ov);
     std::string fn = "hip_conv__" + op.tag;
     rtc->compile({{fn, "", {}, fo}}, rtc_compile_opts_t());
     std::map<std::string, rtc_arg_t> args{{"in", op.bots[0]}, {"filts", fv}, {"out", ov}};
     if (bias) args["biases"] = bv;
+    if (ra != resadds.end()) args["res"] = ra->second.res;
     if (pack_filts && !ip) {
       // Boda's xpose_filts at init (src/rtc_fwd.cc:306-326): the k-major bank the ring kernels read
       std::string xv = op.tag + "_filts_xp";
@@ -651,6 +698,7 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     return;
   }
   if (op.type == "Eltwise") {
+    if (res_fused.count(op.tag)) return;  // in its producing conv's epilogue
     if (op.bots.size() != 2) unsup_err("Eltwise '" + op.tag + "' with " + std::to_string(op.bots.size()) + " inputs");
     if (op.tops[0] != op.bots[0] && op.tops[0] != op.bots[1]) ensure_out(op.tops[0]);
     const uint32_t code = op.eltwise_op == "PROD" ? 0 : (op.eltwise_op == "SUM" ? 1 : 2);
@@ -678,6 +726,7 @@ void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, p_rtc_compute_t const &rtc_
     declared.insert(in);
   }
   if (fold_affines) plan_folds();
+  if (fuse_residual) plan_resadds();
   if (concat_in_place) plan_slabs();
   for (auto const &op : cp->ops) gen_op(*op);
   rtc->finish_and_sync();

@@ -221,7 +221,15 @@ struct hip_compute_t : public rtc_compute_t {
       int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
       // filts_xp (optional): the bank hip_xpose_filts made before the timed calls
       auto oc0 = fi.op.scalars.find("out_chan_ofs");
-      if (oc0 == fi.op.scalars.end()) {
+      float *res = arg_ptr(rfc, "res", true);
+      if (res) {  // residual add (a fused Eltwise SUM) in the conv epilogue
+        if (oc0 != fi.op.scalars.end()) rt_err(fn + ": residual and channel slab together");
+        if (arg_dims(rfc, "res") != arg_dims(rfc, "out")) rt_err(fn + ": res / out dims differ");
+        bh_check(bh_conv2d_fwd_nchw_res(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
+                                        arg_ptr(rfc, "biases", true), res, arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W,
+                                        s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
+                 "hip_conv");
+      } else if (oc0 == fi.op.scalars.end()) {
         bh_check(bh_conv2d_fwd_nchw_pk(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
                                        arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
                                        s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),

@@ -11,6 +11,8 @@
 // --no-fold runs BatchNorm / Scale as separate affine layers instead of folding them into the
 // producing conv (conv_pipe_fwd_t::plan_folds); --no-inplace-concat copies every Concat input
 // instead of letting its producing conv write the Concat's channel slab (plan_slabs).
+// --no-resadd runs a ResNet shortcut Eltwise SUM as its own layer instead of in the epilogue
+// of the conv producing one of its inputs (plan_resadds).
 // --graph R also times the whole forward captured as one hipGraph, replayed R times (ms per
 // forward with every launch seam; the per-layer list is event-timed per call).
 // --save writes DIR/in.f32 and DIR/out.f32 (raw little-endian fp32) for the parity tests.
@@ -86,7 +88,7 @@ int main(int argc, char **argv) {
   std::string net, out_node, save;
   uint32_t img = 0, iters = 3;
   int device = 0;
-  bool plan = false, plan_js = false, plan_exec = false, pack = true, fold = true, inplace = true;
+  bool plan = false, plan_js = false, plan_exec = false, pack = true, fold = true, inplace = true, resadd = true;
   uint32_t graph_reps = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -108,6 +110,7 @@ int main(int argc, char **argv) {
     else if (a == "--plan-exec") plan_exec = true;
     else if (a == "--no-pack") pack = false;
     else if (a == "--no-fold") fold = false;
+    else if (a == "--no-resadd") resadd = false;
     else if (a == "--graph") graph_reps = (uint32_t)atoi(val().c_str());
     else if (a == "--no-inplace-concat") inplace = false;
     else {
@@ -117,7 +120,7 @@ int main(int argc, char **argv) {
   }
   if (net.empty()) {
     fprintf(stderr, "usage: boda_hip_rtc_fwd --net <prototxt> [--img N] [--out-node n] [--iters K] "
-                    "[--plan|--plan-json|--plan-exec] [--save DIR] [--device d] [--no-pack] [--no-fold] [--no-inplace-concat] [--graph R]\n");
+                    "[--plan|--plan-json|--plan-exec] [--save DIR] [--device d] [--no-pack] [--no-fold] [--no-inplace-concat] [--no-resadd] [--graph R]\n");
     return 2;
   }
   try {
@@ -126,6 +129,7 @@ int main(int argc, char **argv) {
       conv_pipe_fwd_t fwd;
       fwd.cp = cp;
       if (fold) fwd.plan_folds();
+      if (resadd) fwd.plan_resadds();
       if (inplace) fwd.plan_slabs();
       printf("%s", fwd.exec_plan_str().c_str());
       return 0;
@@ -145,6 +149,7 @@ int main(int argc, char **argv) {
     fwd.pack_filts = pack;
     fwd.fold_affines = fold;
     fwd.concat_in_place = inplace;
+    fwd.fuse_residual = resadd;
     fwd.init(cp, rtc);
     auto in = std::make_shared<nda_t>(cp->node_dims.at(cp->inputs[0]));
     for (uint64_t i = 0; i < in->dims.elems(); ++i) in->elems()[i] = det_hash_rand((uint32_t)i + 234234567u);

@@ -161,6 +161,16 @@ int bh_conv2d_fwd_nchw_pk(bh_ctx *ctx, const float *in, const float *filts, cons
  * a Concat writes its slab of the Concat's output in place, so the net executor runs no
  * channel copy for it (the reference's conv_pipe_fwd_t copies every Concat input with
  * copy.cucl, src/rtc_fwd.cc:267-280). */
+/* bh_conv2d_fwd_nchw_pk with a residual: out = relu?(conv + bias + res), res B x OC x OH x OW
+ * (may be NULL; may not overlap out unless equal to it). The add is the conv's epilogue, in the
+ * order of a separate Caffe Eltwise SUM of the stored conv output and res (bit-identical to
+ * it): the net executor folds a ResNet shortcut Eltwise (+ its ReLU) into the conv producing
+ * one of its inputs. The reference runs Eltwise as its own layer only in Caffe (its rtc_fwd
+ * rejects it, src/rtc_fwd.cc:404). */
+int bh_conv2d_fwd_nchw_res(bh_ctx *ctx, const float *in, const float *filts, const float *packed,
+                           const float *biases, const float *res, float *out, uint32_t B, uint32_t IC,
+                           uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
+                           uint32_t sx, uint32_t py, uint32_t px, int relu);
 int bh_conv2d_fwd_nchw_slab(bh_ctx *ctx, const float *in, const float *filts, const float *packed,
                             const float *biases, float *out, uint32_t out_chans_total,
                             uint32_t out_chan_ofs, uint32_t B, uint32_t IC, uint32_t H, uint32_t W,
