@@ -173,3 +173,29 @@ def test_conv_writes_channel_slab(dev, s):
         x.free()
     np.testing.assert_array_equal(got[:, ofs:ofs + s.OC], ref)
     assert (got[:, :ofs] == -7.25).all() and (got[:, ofs + s.OC:] == -7.25).all()
+
+
+@pytest.mark.parametrize("s", SLAB_SHAPES, ids=lambda s: "x".join(map(str, s.as_dims())))
+@pytest.mark.parametrize("relu", [0, 1])
+def test_conv_residual_epilogue(dev, s, relu):
+    """bh_conv2d_fwd_nchw_res: out = relu?(conv + bias + res) bit-identical to the plain conv's
+    stored output plus res, rounded once more (what a separate Eltwise SUM computes)."""
+    plain = run_conv(dev, s, relu=0)
+    n = s.B * s.OC * s.OH * s.OW
+    r = (np.random.default_rng(7).standard_normal(n) * 3).astype(np.float32)
+    i = dev.alloc_floats(s.B * s.IC * s.H * s.W)
+    f = dev.alloc_floats(s.OC * s.K)
+    b = dev.alloc_floats(s.OC)
+    dr, o = dev.alloc_floats(n), dev.alloc_floats(n)
+    dev.gen_data(GEN_CONV_IN, i, [s.B, s.IC, s.H, s.W], 5)
+    dev.gen_data(GEN_CONV_FILTS, f, [s.OC, s.IC, s.KY, s.KX], 5)
+    dev.gen_data(GEN_CONV_BIASES, b, [s.OC], 5)
+    dr.upload(r)
+    dev.conv_res(i, f, b, dr, o, s, relu)
+    got = o.download()
+    for x in (i, f, b, dr, o):
+        x.free()
+    exp = (plain + r).astype(np.float32)
+    if relu:
+        exp = np.where(exp < 0, np.float32(0), exp)
+    np.testing.assert_array_equal(got, exp)

@@ -101,3 +101,16 @@ def test_forward_graph_replay(net, tmp_path):
     np.testing.assert_array_equal(g1, g2)
     line = [l for l in log.splitlines() if l.startswith("forward as one hipGraph")]
     assert len(line) == 1 and float(line[0].split(")")[1].split()[0]) > 0, log
+
+
+def test_resnet_residual_in_conv_epilogue_same_bits(tmp_path):
+    """Shortcut Eltwise SUM (+ ReLU) in the producing conv's epilogue (plan_resadds): no eltwise
+    kernel runs, and the output bits equal the executor running Eltwise as its own layer."""
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _, _, g1, log1 = run_net("resnet-50", 2, a)
+    _, _, g2, log2 = run_net("resnet-50", 2, b, ["--no-resadd"])
+    assert "hip_eltwise__" not in log1 and log2.count("hip_eltwise__") == 16
+    np.testing.assert_array_equal(g1, g2)

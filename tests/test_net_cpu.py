@@ -94,9 +94,15 @@ def exec_plan(net, *extra):
 def test_exec_plan_folds_and_slabs():
     """The executor's rewrites (conv_pipe_fwd_t::plan_folds / plan_slabs), planned on the host."""
     r = exec_plan("resnet-50")
-    assert len(r) == 106 and all(l.startswith("fold ") for l in r)  # every BatchNorm and Scale
+    folds = [l for l in r if l.startswith("fold ")]
+    res = [l for l in r if l.startswith("resadd ")]
+    assert len(folds) == 106 and len(res) == 16 and len(r) == 122  # every BatchNorm / Scale, every shortcut sum
     assert "fold BatchNorm bn_conv1 -> conv1" in r and "fold Scale scale_conv1 -> conv1" in r
+    assert "resadd res2a -> res2a_branch2c +relu" in r and "resadd res5c -> res5c_branch2c +relu" in r
+    assert exec_plan("resnet-50", "--no-fold", "--no-resadd") == []
+    # without folding, the conv before each shortcut sum is followed by its BatchNorm: no resadd
     assert exec_plan("resnet-50", "--no-fold") == []
+    assert len(exec_plan("resnet-50", "--no-resadd")) == 106
     g = exec_plan("googlenet_conv")
     assert len(g) == 36 and all(l.startswith("slab ") for l in g)  # 9 Concats x 4 conv inputs
     assert "slab icp1_out1 -> icp2_in @64" in g
