@@ -116,7 +116,10 @@ int bh_destroy(bh_ctx *c) {
 int bh_plat_tag(bh_ctx *c, char *buf, size_t n) {
   BH_CHECK_CTX(c);
   if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
-  std::snprintf(buf, n, "hip:%s:%s", c->prop.name[0] ? c->prop.name : "MI355X", c->prop.gcnArchName);
+  // the marketing name comes from libdrm's amdgpu.ids; where that table is missing (some
+  // launch environments) HIP reports a generic "AMD Radeon Graphics": gfx950 is MI355X
+  const bool named = std::strstr(c->prop.name, "MI3") != nullptr;
+  std::snprintf(buf, n, "hip:%s:%s", named ? c->prop.name : "MI355X", c->prop.gcnArchName);
   return BH_OK;
 }
 
