@@ -9,73 +9,56 @@
 
 namespace {
 
-// Pooling (test/rtc/pool.cucl): a thread per PO output elements; only non-padding pixels
+// Pooling (test/rtc/pool.cucl): one thread per output element; only non-padding pixels
 // count, for max and for average (the average divides by the number of in-image taps).
 // out_in_yx (may be null): for max pooling, the in_y*W + in_x of the winning input (-1 if
 // none), stored as a float as the reference does.
 // KY_/KX_ > 0: the window is a compile-time constant (3x3 and 2x2: every pooling layer of
 // the reference nets but the global ones), so the loop unrolls and all taps' loads issue
-// together instead of one guarded load per loop trip. PO outputs per thread (i, i + S, ...,
-// S = the grid's thread count), computed as independent straight-line code so all PO * taps
-// loads are in flight at once: with one output per thread a big pooling layer ran as ~8
-// back-to-back occupancy rounds each paying a full memory latency (GoogLeNet pool1 at b20:
-// 30 us for 80 MB, 2.7 TB/s).
-template <int KY_, int KX_, int PO>
+// together instead of one guarded load per loop trip.
+template <int KY_, int KX_>
 __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                    float *__restrict__ out_in_yx, uint32_t total, uint32_t C,
                                                    uint32_t H, uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY_rt,
                                                    uint32_t KX_rt, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
                                                    int avg, uint32_t ow_m, uint32_t ow_s, uint32_t oh_m, uint32_t oh_s) {
   const uint32_t KY = KY_ > 0 ? (uint32_t)KY_ : KY_rt, KX = KX_ > 0 ? (uint32_t)KX_ : KX_rt;
-  const uint32_t i0 = blockIdx.x * 256 + threadIdx.x, S = gridDim.x * 256;
-  float v[PO];
-  int oyx[PO];
-#pragma unroll
-  for (int q = 0; q < PO; ++q) {
-    // past the end: compute a valid output (the last) and don't store it
-    const uint32_t i = min(i0 + (uint32_t)q * S, total - 1);
-    // i -> (nc, oy, ox) with multiply-shift division (nc = img * C + chan)
-    const uint32_t t = (__umulhi(i, ow_m) + i) >> ow_s, ox = i - t * OW;
-    const uint32_t nc = (__umulhi(t, oh_m) + t) >> oh_s, oy = t - nc * OH;
-    const float *const src = in + (size_t)nc * H * W;
-    float acc = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
-    int arg = -1;
-    // the reference's loop order (kx outer, ky inner) decides ties and the summation order;
-    // a tap in the padding loads src[0] (always valid) and is then ignored: no guarded load
-    auto tap = [&](uint32_t ky, uint32_t kx) {
-      const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
-      const bool ok = iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H;
-      const float x = src[ok ? iy * (int)W + ix : 0];
-      if (ok) {
-        if (avg) {
-          acc += x;
-          cnt += 1.0f;
-        } else if (x > acc) {
-          acc = x;
-          arg = iy * (int)W + ix;
-        }
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  // i -> (nc, oy, ox) with multiply-shift division (nc = img * C + chan)
+  const uint32_t t = (__umulhi(i, ow_m) + i) >> ow_s, ox = i - t * OW;
+  const uint32_t nc = (__umulhi(t, oh_m) + t) >> oh_s, oy = t - nc * OH;
+  const float *const src = in + (size_t)nc * H * W;
+  float v = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
+  int oyx = -1;
+  // the reference's loop order (kx outer, ky inner) decides ties and the summation order; a
+  // tap in the padding loads src[0] (always valid) and is then ignored, so no load is guarded
+  auto tap = [&](uint32_t ky, uint32_t kx) {
+    const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
+    const bool ok = iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H;
+    const float x = src[ok ? iy * (int)W + ix : 0];
+    if (ok) {
+      if (avg) {
+        v += x;
+        cnt += 1.0f;
+      } else if (x > v) {
+        v = x;
+        oyx = iy * (int)W + ix;
       }
-    };
-    if constexpr (KY_ > 0 && KX_ > 0) {
-#pragma unroll
-      for (int kx = 0; kx < KX_; ++kx)
-#pragma unroll
-        for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
-    } else {
-      for (uint32_t kx = 0; kx < KX; ++kx)
-        for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
     }
-    v[q] = avg ? acc / cnt : acc;
-    oyx[q] = arg;
-  }
+  };
+  if constexpr (KY_ > 0 && KX_ > 0) {
 #pragma unroll
-  for (int q = 0; q < PO; ++q) {
-    const uint32_t i = i0 + (uint32_t)q * S;
-    if (i < total) {
-      out[i] = v[q];
-      if (out_in_yx) out_in_yx[i] = (float)oyx[q];
-    }
+    for (int kx = 0; kx < KX_; ++kx)
+#pragma unroll
+      for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
+  } else {
+    for (uint32_t kx = 0; kx < KX; ++kx)
+      for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
   }
+  if (avg) v /= cnt;
+  out[i] = v;
+  if (out_in_yx) out_in_yx[i] = (float)oyx;
   (void)C;
 }
 
@@ -243,12 +226,10 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
   uint32_t ow_m = fow.m, ow_s = fow.s, oh_m = foh.m, oh_s = foh.s;
   void *args[] = {&in,  &out, &out_in_yx, &tot, &C,   &H,   &W,   (void *)&OH, (void *)&OW, &KY,
                   &KX,  &sy,  &sx,        &py,  &px,  &avg, &ow_m, &ow_s,      &oh_m,       &oh_s};
-  const bool k3 = KY == 3 && KX == 3, k2 = KY == 2 && KX == 2;
-  const uint32_t po = (k3 || k2) ? 4 : 1;  // outputs per thread
-  const void *kern = k3 ? (const void *)pool_kernel<3, 3, 4>
-                        : (k2 ? (const void *)pool_kernel<2, 2, 4> : (const void *)pool_kernel<0, 0, 1>);
-  const uint32_t grid = (uint32_t)(((uint64_t)tot + 256ull * po - 1) / (256ull * po));
-  return launch(ctx, kern, dim3(grid), dim3(256), args, true, true, "pool");
+  const void *kern = KY == 3 && KX == 3   ? (const void *)pool_kernel<3, 3>
+                     : KY == 2 && KX == 2 ? (const void *)pool_kernel<2, 2>
+                                          : (const void *)pool_kernel<0, 0>;
+  return launch(ctx, kern, dim3((tot + 255) / 256), dim3(256), args, true, true, "pool");
 }
 
 int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
