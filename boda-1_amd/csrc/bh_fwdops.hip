@@ -62,68 +62,6 @@ __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in,
   (void)C;
 }
 
-// Row-staged pooling for planes with wide rows: a block owns PR_R consecutive output rows of
-// one plane (a wave per row); the input rows their windows touch are one contiguous span of
-// the plane, staged into LDS by coalesced loads, and the taps (same order, same padding rule
-// as pool_kernel: identical results) read LDS. PMC on pool_kernel (GoogLeNet pool1, b20):
-// waves waiting 78 % of their cycles on nine stride-sx gathers per output, L2 hit rate 50 %
-// (every input line fetched twice), 30 us for 80 MB.
-constexpr int PR_R = 4;          // output rows per block
-constexpr int PR_LDS = 12288;    // staged input floats (48 KB)
-template <int KY_, int KX_>
-__global__ __launch_bounds__(256) void pool_rows_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                        float *__restrict__ out_in_yx, uint32_t H, uint32_t W,
-                                                        uint32_t OH, uint32_t OW, uint32_t KY_rt, uint32_t KX_rt,
-                                                        uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int avg,
-                                                        uint32_t n_oyg) {
-  __shared__ float rows[PR_LDS];
-  const uint32_t KY = KY_ > 0 ? (uint32_t)KY_ : KY_rt, KX = KX_ > 0 ? (uint32_t)KX_ : KX_rt;
-  const uint32_t nc = blockIdx.x / n_oyg, oy0 = (blockIdx.x - nc * n_oyg) * PR_R;
-  const uint32_t nr = min((uint32_t)PR_R, OH - oy0);
-  // input rows [iy_lo, iy_hi) of this block's windows, clipped to the plane
-  const int iy_lo = max(0, (int)(oy0 * sy) - (int)py);
-  const int iy_hi = min((int)H, (int)((oy0 + nr - 1) * sy + KY) - (int)py);
-  const float *const src = in + (size_t)nc * H * W + (size_t)iy_lo * W;
-  const int n = iy_hi > iy_lo ? (iy_hi - iy_lo) * (int)W : 0;
-  for (int i = threadIdx.x; i < n; i += 256) rows[i] = src[i];
-  __syncthreads();
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave >= nr) return;
-  const uint32_t oy = oy0 + wave;
-  float *const orow = out + ((size_t)nc * OH + oy) * OW;
-  float *const arow = out_in_yx ? out_in_yx + ((size_t)nc * OH + oy) * OW : nullptr;
-  for (uint32_t ox = lane; ox < OW; ox += 64) {
-    float acc = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
-    int arg = -1;
-    auto tap = [&](uint32_t ky, uint32_t kx) {
-      const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
-      const bool ok = iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H;
-      const float x = rows[ok ? (iy - iy_lo) * (int)W + ix : 0];
-      if (ok) {
-        if (avg) {
-          acc += x;
-          cnt += 1.0f;
-        } else if (x > acc) {
-          acc = x;
-          arg = iy * (int)W + ix;
-        }
-      }
-    };
-    // the reference's loop order (kx outer, ky inner), as pool_kernel
-    if constexpr (KY_ > 0 && KX_ > 0) {
-#pragma unroll
-      for (int kx = 0; kx < KX_; ++kx)
-#pragma unroll
-        for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
-    } else {
-      for (uint32_t kx = 0; kx < KX; ++kx)
-        for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
-    }
-    orow[ox] = avg ? acc / cnt : acc;
-    if (arow) arow[ox] = (float)arg;
-  }
-}
-
 // LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): a running sum of squares over a
 // window of LS channels kept with a ring of the last LS inputs (+ new^2 - old^2, the
 // reference's order), out = in * (k + alpha/LS * sum)^-beta.
@@ -288,18 +226,6 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
   uint32_t ow_m = fow.m, ow_s = fow.s, oh_m = foh.m, oh_s = foh.s;
   void *args[] = {&in,  &out, &out_in_yx, &tot, &C,   &H,   &W,   (void *)&OH, (void *)&OW, &KY,
                   &KX,  &sy,  &sx,        &py,  &px,  &avg, &ow_m, &ow_s,      &oh_m,       &oh_s};
-  const uint64_t span = (uint64_t)((PR_R - 1) * sy + KY) * W;  // staged floats per block (upper bound)
-  if (OW >= 16 && span <= (uint64_t)PR_LDS) {  // wide rows: row-staged kernel
-    uint32_t n_oyg = (OH + PR_R - 1) / PR_R;
-    const uint64_t blocks = (uint64_t)B * C * n_oyg;
-    if (blocks < (1ull << 31)) {
-      void *ra[] = {&in, &out, &out_in_yx, &H, &W, (void *)&OH, (void *)&OW, &KY, &KX, &sy, &sx, &py, &px, &avg, &n_oyg};
-      const void *rk = KY == 3 && KX == 3   ? (const void *)pool_rows_kernel<3, 3>
-                       : KY == 2 && KX == 2 ? (const void *)pool_rows_kernel<2, 2>
-                                            : (const void *)pool_rows_kernel<0, 0>;
-      return launch(ctx, rk, dim3((uint32_t)blocks), dim3(256), ra, true, true, "pool");
-    }
-  }
   const void *kern = KY == 3 && KX == 3   ? (const void *)pool_kernel<3, 3>
                      : KY == 2 && KX == 2 ? (const void *)pool_kernel<2, 2>
                                           : (const void *)pool_kernel<0, 0>;

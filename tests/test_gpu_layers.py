@@ -29,9 +29,9 @@ POOLS = [  # B, C, H, W, KY, KX, sy, sx, py, px, avg
     (3, 1024, 7, 7, 7, 7, 1, 1, 0, 0, 1),    # GoogLeNet global average pool
     (2, 7, 9, 11, 3, 2, 2, 3, 1, 1, 1),      # ragged, padded average
     (1, 3, 5, 5, 4, 4, 3, 3, 2, 2, 0),       # partial windows at both ends
-    (2, 5, 40, 37, 3, 3, 1, 1, 1, 1, 1),     # row-staged kernel (OW >= 16): padded average, stride 1
-    (2, 3, 30, 41, 2, 2, 2, 2, 0, 0, 0),     # row-staged, 2x2 (VGG-style), partial last column
-    (1, 2, 19, 70, 5, 4, 3, 3, 2, 1, 0),     # row-staged, runtime window, partial last row
+    (2, 5, 40, 37, 3, 3, 1, 1, 1, 1, 1),     # wide rows: padded average, stride 1
+    (2, 3, 30, 41, 2, 2, 2, 2, 0, 0, 0),     # 2x2 (VGG-style), partial last column
+    (1, 2, 19, 70, 5, 4, 3, 3, 2, 1, 0),     # runtime window, partial last row
 ]
 
 
