@@ -99,6 +99,8 @@ def main():
                     "only if the new best is this much faster (timings vary a few %% from box to box)")
     ap.add_argument("--cfg-re", default="", help="sweep only configs matching this regex (plus the --out "
                     "table's current choice for the op, timed again, so the better one is kept)")
+    ap.add_argument("--only-untuned", action="store_true", help="sweep only ops the --out table has no entry "
+                    "for (use with --merge)")
     args = ap.parse_args()
     global TIMING
     TIMING = args.timing
@@ -113,6 +115,9 @@ def main():
             m = re.match(r"(.*) cfg=(\S+) splits=(\d+) red=(\w)", l)
             if m:
                 prev[m.group(1)] = (m.group(2), int(m.group(3)) * (-1 if m.group(4) == "k" else 1))
+    have = set()
+    if args.only_untuned and os.path.exists(args.out):
+        have = {l[:l.index(" cfg=")] for l in open(args.out) if " cfg=" in l and not l.startswith("#")}
     t_start = time.time()
     for sname in args.sets.split(","):
         o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", SETS[sname]))
@@ -125,7 +130,7 @@ def main():
             kind = 0 if isinstance(s, ops.SgemmShape) else 1
             dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
             key = ("sgemm " if kind == 0 else "conv ") + " ".join(map(str, dims))
-            if key in table:
+            if key in table or key in have:
                 continue
             wl = runner.Workload(dev, [s])
             M, N, K = (s.M, s.N, s.K) if kind == 0 else (s.OC, s.B * s.OH * s.OW, s.K)
