@@ -101,7 +101,10 @@ __global__ __launch_bounds__(256) void lrn_kernel(const float *__restrict__ in, 
     if (j >= 2 * hls && oc < (int)C) {
       const float sb = k + sum * alpha_over_ls;
       if (out_scale_base) out_scale_base[base + (size_t)oc * HW] = sb;
-      out[base + (size_t)oc * HW] = x[j - hls] * powf(sb, -beta);
+      // sb^-beta as exp2(-beta * log2(sb)) on the hardware transcendentals (v_log_f32 /
+      // v_exp_f32): what the reference's kernels get from nvrtc --use_fast_math (__powf,
+      // src/nvrtc_util.cc:251); an accurate powf made this layer instruction-latency bound
+      out[base + (size_t)oc * HW] = x[j - hls] * __builtin_amdgcn_exp2f(-beta * __builtin_amdgcn_logf(sb));
     }
   }
 }
