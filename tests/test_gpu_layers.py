@@ -63,7 +63,8 @@ def test_lrn(dev, p):
     dx, do, ds = _up(dev, x), dev.alloc_floats(x.size), dev.alloc_floats(x.size)
     dev.lrn(dx, do, B, C, H, W, ls, alpha, beta, k, out_scale_base=ds)
     # fma contraction, and channel chunks past the first starting their running sum fresh
-    # (bh_fwdops.hip lrn_kernel; the reference sum carries +/- residue of earlier channels): < 2e-6
+    # (bh_fwdops.hip lrn_kernel; the reference sum carries +/- residue of earlier channels): < 2e-6;
+    # out also carries the hardware exp2/log2 for scale^-beta (the reference's fast-math __powf)
     np.testing.assert_allclose(ds.download().reshape(x.shape), sb, rtol=2e-6, atol=0)
     np.testing.assert_allclose(do.download().reshape(x.shape), ref, rtol=2e-6, atol=1e-30)
     for b in (dx, do, ds):
