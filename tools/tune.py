@@ -30,7 +30,9 @@ import boda_hip  # noqa: E402
 from boda_hip import ops, runner  # noqa: E402
 
 SETS = {"sgemm-full": "sgemm-ops-full.txt", "sgemm-small": "sgemm-ops-small.txt",
-        "conv": "conv-ops-1-5-20-nin-alex-gn.txt", "op-sigs": "op_sigs_full.txt"}
+        "conv": "conv-ops-1-5-20-nin-alex-gn.txt", "op-sigs": "op_sigs_full.txt",
+        # the conv / fc shapes of the five reference nets at batch 20 (tools/net_ops.py)
+        "nets": os.path.join(ROOT, "boda-1_amd", "tuning", "net-ops-b20.txt")}
 SPLITS = [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 32, 48, 64]
 CFG_BK = {}
 
@@ -120,7 +122,7 @@ def main():
         have = {l[:l.index(" cfg=")] for l in open(args.out) if " cfg=" in l and not l.startswith("#")}
     t_start = time.time()
     for sname in args.sets.split(","):
-        o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", SETS[sname]))
+        o, _ = ops.read_ops(os.path.join(ROOT, "tests", "golden", "ops", SETS[sname]))  # (absolute: as is)
         shapes = []
         for op in o:
             s = ops.shape_of(op)
