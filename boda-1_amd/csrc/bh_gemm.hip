@@ -897,7 +897,9 @@ void load_tuning() {
   fclose(f);
 }
 
-choice_t heuristic(int op, const uint32_t *d) {
+// Kernel choice for shapes the tuning table lacks. ring = false: no ring (LDS-DMA, packed
+// bank) config -- launch_conv's fallback when the bank or input is too large for it.
+choice_t heuristic(int op, const uint32_t *d, bool ring = true) {
   choice_t ch;
   if (op == 0) {
     ch.cfg = 0;
@@ -913,6 +915,9 @@ choice_t heuristic(int op, const uint32_t *d) {
   if (N <= 64 && (uint64_t)OC * K >= (1u << 20) && K % 4 == 0) n = N <= 16 ? "gv64x16" : (N <= 32 ? "gv64x32" : "gv32x64");
   else if (N <= 32) n = "128x32x32";
   else if (OC <= 32) n = "32x256x32";
+  // big convs: the ring kernels, as the tuner picks them for the nets' shapes (VGG-19 / ResNet-50
+  // at b20, profiles/r01/nets/tune_nets_b20.log: 128x128 ring on big grids, 64-row rings below)
+  else if (ring && K >= 256 && N >= 1024) n = tiles128 >= 256 ? "r128x128x32d2" : (OC <= 64 ? "r64x128x32d3" : "r64x64x32d3");
   else if (OC <= 64) n = "64x128x32";
   else if (tiles128 < 256 && K >= 256) n = "128x32x32";
   ch.cfg = cfg_index(1, n);
@@ -1178,7 +1183,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     const uint32_t oc4 = (OC + 3) & ~3u, kp = (uint32_t)(pk_floats / oc4);
     const float *wp = packed;
     if (pk_floats * 4 >= 0x7fffffc0ull || in_bytes >= (1ull << 30)) {
-      ch = heuristic(1, d);
+      ch = heuristic(1, d, false);
     } else {
       if (!wp) {
         int rc = ensure_wpack(ctx, pk_floats * 4);
