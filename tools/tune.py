@@ -32,7 +32,9 @@ from boda_hip import ops, runner  # noqa: E402
 SETS = {"sgemm-full": "sgemm-ops-full.txt", "sgemm-small": "sgemm-ops-small.txt",
         "conv": "conv-ops-1-5-20-nin-alex-gn.txt", "op-sigs": "op_sigs_full.txt",
         # the conv / fc shapes of the five reference nets at batch 20 (tools/net_ops.py)
-        "nets": os.path.join(ROOT, "boda-1_amd", "tuning", "net-ops-b20.txt")}
+        "nets": os.path.join(ROOT, "boda-1_amd", "tuning", "net-ops-b20.txt"),
+        "nets-b1": os.path.join(ROOT, "boda-1_amd", "tuning", "net-ops-b1.txt"),
+        "nets-b5": os.path.join(ROOT, "boda-1_amd", "tuning", "net-ops-b5.txt")}
 SPLITS = [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 32, 48, 64]
 CFG_BK = {}
 
