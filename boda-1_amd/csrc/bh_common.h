@@ -31,6 +31,9 @@ struct bh_ctx {
   uint64_t cnt_n = 0;
   void *wpack = nullptr;  // k-major filter bank for the ring conv kernels, grown on demand
   size_t wpack_bytes = 0;
+  // outgrown workspaces still referenced by captured graphs: freed with the context
+  // (a graph replays the pointers it was captured with)
+  std::vector<void *> retired;
 };
 
 namespace bh {
@@ -72,6 +75,46 @@ inline fastdiv make_fastdiv(uint32_t d) {
 #define BH_CHECK_CTX(c) \
   do { if (!(c)) return bh::fail(BH_ERR, "null bh_ctx"); } while (0)
 
+namespace bh {
+// Every C-ABI entry that allocates, creates events or launches runs with the context's
+// device current (several contexts / host threads may drive several GPUs), restoring the
+// caller's device on return.
+struct device_scope {
+  int prev = -1;
+  explicit device_scope(const bh_ctx *c) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != c->device) (void)hipSetDevice(c->device);
+  }
+  ~device_scope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+// A hot-path call consumes the event pair bh_time_next_call armed, whether it launched or
+// failed first: a pair left armed by a rejected call must not attach to an unrelated later
+// launch.
+struct call_scope : device_scope {
+  bh_ctx *c;
+  explicit call_scope(bh_ctx *ctx) : device_scope(ctx), c(ctx) {}
+  ~call_scope() {
+    c->t_start = nullptr;
+    c->t_stop = nullptr;
+  }
+};
+// Grow a per-context device buffer to at least `want` bytes (+25 % headroom). Refuses to
+// allocate while the context's stream is capturing (a capture records no allocation: run the
+// op once eagerly first). The outgrown buffer is kept until the context is destroyed when a
+// captured graph may still reference it, freed otherwise.
+int grow_buffer(bh_ctx *ctx, void *&buf, size_t &have, size_t want, bool zero, const char *what);
+}  // namespace bh
+
+#define BH_ENTER(c)  \
+  BH_CHECK_CTX(c);   \
+  bh::device_scope bh_dev_scope_(c)
+#define BH_ENTER_CALL(c) \
+  BH_CHECK_CTX(c);       \
+  bh::call_scope bh_call_scope_(c)
+
 // ---- internal entry points implemented in the kernel sources ----
 namespace bh {
 int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi);
@@ -79,7 +122,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
                 float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                 uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0,
-                const float *res = nullptr);
+                const float *res = nullptr, bool no_dc = false);
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX);

@@ -1,0 +1,362 @@
+// bh_direct.hip -- direct convolution for the few-channel, large-kernel stem layers.
+//
+// The stems of the conv set -- 3 x 224^2 -> 64 7x7 s2 (GoogLeNet conv1) and 3 x 227^2 ->
+// 96 11x11 s4 (AlexNet conv1), at batch 1 / 5 / 20 -- are the shapes Boda sends to its tconv
+// variant (test/rtc/tconv.cucl:1-52, chosen at src/cnn_op.cc:60-63: kernel <= 11x11, output
+// width >= 6): a "tiled" direct conv whose input is staged per block. As an implicit GEMM
+// (the ring kernels) they are the wrong shape: K = 3*KY*KX = 147 / 363 is short and every k
+// row of every stage is a separate 64-column gather of a strided input row, so each input
+// pixel is fetched KY*KX/S^2 = 7.6-12 times. Here
+//  * a block owns OCT = 32*TM output channels x NPX = 128*TN consecutive output pixels of one
+//    image (a run that may straddle output rows) and a ring of D stages, one stage per INPUT
+//    CHANNEL: the channel's weights [2*KK2 taps][OCT] (from the packed k-major bank of
+//    bh_conv_filts_pack, 16-B LDS-DMA) and its input strip -- the RIN input rows the block's
+//    pixels touch, whole rows at pitch WPM with the zero padding materialised -- filled once by
+//    coalesced dword LDS-DMA (a row is contiguous in NCHW). Each input element is read from
+//    L2 about once per block instead of once per filter tap;
+//  * MFMA v_mfma_f32_32x32x2_f32 (exact fp32): A = weights (lane i: output channel 32t+i),
+//    B = the strip (lane j: pixel 32*tn+j of the wave). Lane half h takes taps h*KK2+s at step
+//    s; a tap's strip offset ky*WPM+kx is a compile-time constant, the pixel's offset
+//    ((oy-oy_a)*S)*WPM + ox*S a per-lane register, so a B fragment is one ds_read_b32 with an
+//    immediate offset plus one select per step -- no per-element index arithmetic;
+//  * the epilogue adds the bias (staged in LDS by DMA), the optional residual, ReLU, and
+//    stores NCHW rows: 32 consecutive pixels per lane group, 128-B segments.
+// Same GemmArgs contract as the other conv kernels (a = packed bank, lda = OC4; b = input;
+// OCOHW = the output's image stride, so slab outputs work).
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+namespace {
+
+// blocks b, b+8, b+16, ... share an XCD under round-robin placement: give them consecutive
+// pixel tiles (their input strips overlap by the halo rows) -- bijective for any count
+__device__ __forceinline__ uint32_t dc_remap(uint32_t bid, uint32_t n) {
+  const uint32_t xcd = bid & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int KX, int WPM>
+constexpr int dc_koff(int tap, int KK) {
+  return tap < KK ? (tap / KX) * WPM + tap % KX : 0;  // padding taps (zero weights): any in-strip offset
+}
+
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D>
+__global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
+  constexpr int NW = 4;
+  constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
+  constexpr int KK = KY * KX, KK2 = (KK + 1) / 2;
+  constexpr int WPC = 2 * KK2 * OCT / 4;                  // 16-B weight pieces per stage
+  constexpr int LWA = (WPC + NW * 64 - 1) / (NW * 64);    // weight DMA instructions per wave
+  constexpr int WREG = LWA * NW * 256;                    // floats
+  constexpr int SF = RIN * WPM;
+  constexpr int LWB = (SF + NW * 64 - 1) / (NW * 64);     // strip DMA instructions per wave
+  constexpr int SREG = LWB * NW * 64;
+  constexpr int BREG = NW * 64;                           // the stage tile's biases, one DMA per wave
+  constexpr int SLOT = WREG + SREG + BREG;
+  constexpr int LW = LWA + LWB + 1;
+  static_assert(D >= 2 && (D - 2) * LW <= 63, "vmcnt range");
+  static_assert(OCT % 4 == 0 && OCT <= BREG, "16-B weight pieces, biases of one tile");
+  constexpr int PF = TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3);  // LDS fragment prefetch distance (steps)
+  constexpr int IS = (KK2 + 1) / 2 > 1 ? (KK2 + 1) / 2 : 1;     // steps the next stage's DMAs are spread over
+  // C staging: ER rows (a multiple of 8: one 4-register group of every MFMA tile) per pass,
+  // in the slot of the stage just consumed
+  constexpr int ER = (SLOT - BREG) / NPX >= 32 ? 32 : ((SLOT - BREG) / NPX >= 16 ? 16 : 8);
+  static_assert(ER * NPX <= SLOT - BREG, "C staging rows");
+  constexpr int CPP = ER * NPX / 4;  // float4 chunks per staging pass
+  static_assert(CPP % 256 == 0, "chunks per thread");
+  // one __shared__ array only (a second object makes hipcc wait vmcnt(0) at ds_reads)
+  __shared__ __attribute__((aligned(16))) float smem[D * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = lane >> 5, li = lane & 31;
+  KT(0);
+
+  // ---- this block's tiles: t = blockIdx.x + i * gridDim.x; tile t = (pixel run, image, OC tile)
+  // with the OC tile fastest (consecutive tiles share the input strip through L2)
+  const uint32_t G = gridDim.x, b0 = blockIdx.x;
+  const uint32_t ntile = p.total_it;  // tiles of the op
+  const uint32_t my_tiles = b0 < ntile ? (ntile - b0 + G - 1) / G : 0;
+  const uint32_t nstage = my_tiles * p.IC;
+  auto decode = [&](uint32_t t, uint32_t &oc0, uint32_t &img, uint32_t &p0) {
+    const uint32_t rest = fdiv(t, p.ipt_m, p.ipt_s);  // ipt = OC tiles
+    oc0 = (t - rest * p.ipt) * OCT;
+    img = fdiv(rest, p.tm_m, p.tm_s);                // tiles_n = pixel runs per image
+    p0 = (rest - img * p.tiles_n) * NPX;
+  };
+
+  // ---- tile-independent per-lane parts of the DMA source offsets (a stage adds its tile's and
+  // channel's): weight piece e of the [tap][OCT] image = packed-bank row tap*IC + ic (K order
+  // (ky, kx, ic)), column 4*c4; strip element e = (row r, column c) of the [RIN][WPM] image
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+  uint32_t wrel[LWA], wc4[LWA], srel[LWB], srow[LWB];  // wc4 / srow = 0xffff: a piece that never loads
+#pragma unroll
+  for (int j = 0; j < LWA; ++j) {
+    const uint32_t e = (uint32_t)((wave * LWA + j) * 64 + lane);
+    const uint32_t tap = e / (OCT / 4);
+    wc4[j] = tap < (uint32_t)KK ? 4 * (e % (OCT / 4)) : 0xffffu;
+    wrel[j] = (tap * p.IC * p.lda + 4 * (e % (OCT / 4))) * 4u;
+  }
+#pragma unroll
+  for (int j = 0; j < LWB; ++j) {
+    const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
+    const uint32_t r = e / WPM, c = e - (e / WPM) * WPM;
+    const int x = (int)c - (int)p.px;
+    srow[j] = (r < (uint32_t)RIN) & ((uint32_t)x < p.W) ? r : 0xffffu;
+    srel[j] = (r * p.W + (uint32_t)x) * 4u;
+  }
+
+  // Source offsets of this wave's LW DMA instructions for block stage g (tile g / IC, input
+  // channel g % IC); stages past the block's last tile are all misses (OOB zeros, no memory
+  // traffic) so every wave always has the same number in flight and nothing branches
+  auto plan = [&](uint32_t g, uint32_t (&vo)[LW]) {
+    const uint32_t i = fdiv(g, p.ic_m, p.ic_s), ic = g - i * p.IC;
+    uint32_t oc0, img, p0;
+    decode(b0 + i * G, oc0, img, p0);
+    const uint32_t dead = g < nstage ? 0u : OOB;
+    const uint32_t wlim = p.lda - min(oc0, p.lda), wb = (oc0 + ic * p.lda) * 4u;
+#pragma unroll
+    for (int j = 0; j < LWA; ++j) vo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
+    const int ya = (int)(fdiv(p0, p.ow_m, p.ow_s) * S) - (int)p.py;  // input row of strip row 0
+    const uint32_t rlo = (uint32_t)max(0, -ya), rhi = (uint32_t)max(0, (int)p.H - ya);
+    const uint32_t sb = (img * p.ICHW + ic * p.HW) * 4u + (uint32_t)(ya * (int)p.W) * 4u;
+#pragma unroll
+    for (int j = 0; j < LWB; ++j)
+      vo[LWA + j] = oob_unless((srow[j] >= rlo) & (srow[j] < rhi), srel[j] + sb) | dead;
+    vo[LW - 1] = oob_unless((uint32_t)(64 * wave + lane) < (uint32_t)OCT, (oc0 + 64 * wave + lane) * 4u) | dead;
+  };
+  auto issue_one = [&](int q, int slot, uint32_t vo) {
+    float *const base = smem + slot * SLOT;
+    if (q < LWA) dma16(rsw, base + (wave * LWA + q) * 256, vo);
+    else if (q < LWA + LWB) dma4(rsi, base + WREG + (wave * LWB + q - LWA) * 64, vo);
+    else dma4(rsbias, base + WREG + SREG + 64 * wave, vo);
+  };
+
+  f32x16 acc[TM][TN];
+  uint32_t poff[TN];  // this lane's pixels' strip offsets in the current tile (bytes)
+  uint32_t hsel = kh ? 0xffffffffu : 0u;
+
+  // one stage = one input channel of one tile: KK2 steps of TM x TN MFMAs; stage g_issue's
+  // DMAs are issued over the first IS steps; LDS fragments are read PF steps ahead
+  auto compute = [&](int slot, int islot, uint32_t g_issue) {
+    uint32_t vo[LW];
+    plan(g_issue, vo);
+    const float *const Ab = smem + slot * SLOT + kh * KK2 * OCT + li;
+    const char *const Sb = (const char *)(smem + slot * SLOT + WREG);
+    // opaque per stage: otherwise hipcc hoists every step's (lane half -> tap offset) select out
+    // of the stage loop and keeps KK2 of them live
+    asm volatile("" : "+v"(hsel));
+    auto frag = [&](int s, float (&a)[TM], float (&b)[TN]) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a[t] = Ab[s * OCT + 32 * t];
+      const uint32_t k0 = (uint32_t)dc_koff<KX, WPM>(s, KK) * 4u;
+      const uint32_t dk = (uint32_t)(dc_koff<KX, WPM>(KK2 + s, KK) - dc_koff<KX, WPM>(s, KK)) * 4u;
+      const uint32_t ko = k0 + (hsel & dk);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(Sb + poff[tn] + ko);
+    };
+    float a[PF + 1][TM], b[PF + 1][TN];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) frag(s, a[s], b[s]);
+#pragma unroll
+    for (int s = 0; s < KK2; ++s) {
+      if (s + PF < KK2) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s % (PF + 1)][t], b[s % (PF + 1)][tn], acc[t][tn], 0, 0, 0);
+      // q in [QB(s), QB(s+1)), QB(s) = ceil(s * LW / IS): early, so that even the last DMA has
+      // most of a stage to land before the wait that retires it (the very next stage at D = 2)
+#pragma unroll
+      for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
+        issue_one(q, islot, vo[q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- prologue: stages 0 .. D-2 in flight
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) {
+    uint32_t vo[LW];
+    plan((uint32_t)s, vo);
+#pragma unroll
+    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+  }
+  const bool vec = p.cvec != 0;
+  int slot = 0;
+  uint32_t g = 0;
+  // outer loop over the block's tiles, inner over a tile's input channels (nested: the
+  // accumulators stay in AGPRs); the ring runs on across tiles, so the next tile's first stage
+  // lands while this tile's epilogue stores go out
+  for (uint32_t i = 0; i < my_tiles; ++i) {
+    uint32_t oc0, img, p0;
+    decode(b0 + i * G, oc0, img, p0);
+    const uint32_t oy_a = fdiv(p0, p.ow_m, p.ow_s);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const uint32_t px = p0 + (uint32_t)(wave * 32 * TN + 32 * tn + li);
+      const uint32_t oy = fdiv(px, p.ow_m, p.ow_s), ox = px - oy * p.OW;
+      poff[tn] = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S) * 4u : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][tn][r] = 0.0f;
+    int cslot = 0;
+    for (uint32_t ic = 0; ic < p.IC; ++ic, ++g) {
+      vm_wait<(D - 2) * LW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage g landed for all waves; all done reading g-1
+      asm volatile("" ::: "memory");
+      if (i == 0 && ic == 0) KT(1);
+      compute(slot, slot == 0 ? D - 1 : slot - 1, g + D - 1);  // + stage g+D-1 into slot (g-1) % D
+      cslot = slot;
+      slot = slot == D - 1 ? 0 : slot + 1;
+    }
+    if (i == 0) KT(2);
+
+    // ---- epilogue through LDS, in the slot of the stage just consumed (no DMA targets it
+    // before the next stage's compute): ER rows of every MFMA tile at a time are written by
+    // fragment, then read back row-major and stored as 16-B pieces -- a wave instruction
+    // writes one 1-KB output row run, a quarter of the store instructions of per-fragment
+    // dword stores (the store issue bounds such an epilogue: cdna_hip_programming.md T21)
+    float *const Cs = smem + cslot * SLOT;
+    const float *const Lb = smem + cslot * SLOT + WREG + SREG;
+    const size_t obase = (size_t)img * p.OCOHW;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+#pragma unroll
+      for (int h = 0; h < 32 / ER; ++h) {
+        // raw barriers: a __syncthreads() would also wait (vmcnt(0)) for the next stage's DMAs
+        // and this epilogue's own stores, which may stay in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is done reading the slot (stage operands / previous pass)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int r = h * (ER / 2); r < (h + 1) * (ER / 2); ++r)
+            Cs[((r & 3) + 8 * (r >> 2) + 4 * kh - h * ER) * NPX + wave * 32 * TN + 32 * tn + li] = acc[t][tn][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < CPP / 256; ++j) {
+          const int c = tid + 256 * j, row = c / (NPX / 4), col = 4 * (c % (NPX / 4));
+          const int trow = 32 * t + h * ER + row;
+          const uint32_t m = oc0 + (uint32_t)trow, px = p0 + (uint32_t)col;
+          if (m < p.M && px < p.OHW) {
+            f32x4v v = *(const f32x4v *)&Cs[row * NPX + col];
+            const float bb = Lb[trow];
+            const size_t o = obase + (size_t)m * p.OHW + px;
+            if (vec && px + 4 <= p.OHW) {
+              v += bb;
+              if (p.res) v += *(const f32x4v *)&p.res[o];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = (p.relu && v[q] < 0.0f) ? 0.0f : v[q];
+              *(f32x4v *)&p.c[o] = v;
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                if (px + q >= p.OHW) break;
+                float x = v[q] + bb;
+                if (p.res) x += p.res[o + q];
+                p.c[o + q] = (p.relu && x < 0.0f) ? 0.0f : x;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  vm_wait<0>();
+#ifdef BH_KTRACE
+  KT(4);
+#endif
+}
+
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D>
+cfg_t dc_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 128 * TN, 2 * ((KY * KX + 1) / 2), 256, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D>;
+  c.dc = 1;
+  c.dc_ky = KY;
+  c.dc_kx = KX;
+  c.dc_s = S;
+  c.dc_wpm = WPM;
+  c.dc_rin = RIN;
+  return c;
+}
+
+}  // namespace
+
+std::vector<cfg_t> dc_cfgs() {
+  return {
+      // GoogLeNet conv1 (3 x 224^2 -> 64, 7x7 s2 p3); 96 channels: the op_sigs 7x7 s2 stem
+      dc_cfg<7, 7, 2, 232, 13, 2, 2, 2>("dc7s2x64d2"),
+      dc_cfg<7, 7, 2, 232, 13, 2, 2, 3>("dc7s2x64d3"),
+      dc_cfg<7, 7, 2, 232, 13, 1, 2, 3>("dc7s2x32d3"),
+      dc_cfg<7, 7, 2, 232, 13, 3, 2, 2>("dc7s2x96d2"),
+      dc_cfg<7, 7, 2, 232, 11, 2, 1, 2>("dc7s2x64n128d2"),
+      // AlexNet conv1 (3 x 227^2 / 224^2 -> 96, 11x11 s4)
+      dc_cfg<11, 11, 4, 228, 23, 3, 1, 2>("dc11s4x96d2"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 2>("dc11s4x32d2"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 3>("dc11s4x32d3"),
+      dc_cfg<11, 11, 4, 228, 31, 1, 2, 2>("dc11s4x32n256d2"),
+      // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
+      dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
+      dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),
+  };
+}
+
+// Launch a direct-conv configuration (p filled by launch_conv with a = packed bank): UNSUP if
+// the shape is not this instantiation's (kernel, stride) or its strip would not fit.
+int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+              uint32_t sx, bool first) {
+  if ((int)KY != c.dc_ky || (int)KX != c.dc_kx || (int)sy != c.dc_s || (int)sx != c.dc_s)
+    return bh::fail(BH_UNSUP, std::string("conv: direct config ") + c.name + " is for another kernel / stride");
+  if (p.W + 2 * p.px > (uint32_t)c.dc_wpm)
+    return bh::fail(BH_UNSUP, std::string("conv: input row too wide for ") + c.name);
+  const uint32_t npx = (uint32_t)c.BN, OW = p.OW, OHW = p.OHW;
+  const uint32_t tiles = (OHW + npx - 1) / npx;
+  // input rows the worst pixel tile touches
+  for (uint32_t t = 0; t < tiles; ++t) {
+    const uint32_t a = t * npx, b = std::min(OHW, a + npx) - 1;
+    if ((b / OW - a / OW) * sy + KY > (uint32_t)c.dc_rin)
+      return bh::fail(BH_UNSUP, std::string("conv: pixel tile spans too many input rows for ") + c.name);
+  }
+  const uint32_t octiles = (p.M + c.BM - 1) / c.BM;
+  const uint64_t ntile = (uint64_t)B * tiles * octiles;
+  if (ntile >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many tiles");
+  // persistent grid: as many blocks as fit on the device at once (each loops over tiles)
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  int bpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k, 256, 0) != hipSuccess || bpc < 1) bpc = 1;
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  const uint32_t G = (uint32_t)std::min<uint64_t>(ntile, (uint64_t)ncu * std::min(bpc, 4));
+  p.total_it = (uint32_t)ntile;
+  p.tiles_n = tiles;
+  p.ipt = octiles;
+  bh::fastdiv f = bh::make_fastdiv(tiles);
+  p.tm_m = f.m;
+  p.tm_s = f.s;
+  f = bh::make_fastdiv(octiles);
+  p.ipt_m = f.m;
+  p.ipt_s = f.s;
+  f = bh::make_fastdiv(OW);
+  p.ow_m = f.m;
+  p.ow_s = f.s;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3(G, 1, 1), dim3(256), args, first, true, "conv_direct");
+}
+
+}  // namespace bhk

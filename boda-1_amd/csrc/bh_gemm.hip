@@ -754,8 +754,10 @@ cfg_t sgemm_cfg(const char *name) {
 // Tile configurations (BM x BN x BK; 32x32 MFMA tiles per wave TM x TN; waves M x N).
 std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
   for (auto const &c : ring_cfgs(op)) v.push_back(c);
-  if (op == 1)
+  if (op == 1) {
     for (auto const &c : gv_cfgs()) v.push_back(c);
+    for (auto const &c : dc_cfgs()) v.push_back(c);
+  }
   return v;
 }
 
@@ -808,33 +810,15 @@ void set_fd(uint32_t d, uint32_t &m, uint32_t &s) {
 }
 
 int ensure_ws(bh_ctx *ctx, size_t bytes) {
-  if (ctx->ws_bytes >= bytes) return BH_OK;
-  if (ctx->ws) {
-    BH_HIP(hipStreamSynchronize(ctx->stream));
-    BH_HIP(hipFree(ctx->ws));
-    ctx->ws = nullptr;
-    ctx->ws_bytes = 0;
-  }
-  size_t want = bytes + (bytes >> 2);
-  BH_HIP(hipMalloc(&ctx->ws, want));
-  ctx->ws_bytes = want;
-  return BH_OK;
+  return bh::grow_buffer(ctx, ctx->ws, ctx->ws_bytes, bytes, false, "split-K workspace");
 }
 
-// split-K arrival tickets: zeroed once at allocation, reset by each tile's last arriver
+// split-K arrival tickets: zeroed at allocation, reset by each tile's last arriver
 int ensure_cnt(bh_ctx *ctx, uint64_t n) {
-  if (ctx->cnt_n >= n) return BH_OK;
-  if (ctx->cnt) {
-    BH_HIP(hipStreamSynchronize(ctx->stream));
-    BH_HIP(hipFree(ctx->cnt));
-    ctx->cnt = nullptr;
-    ctx->cnt_n = 0;
-  }
-  uint64_t want = std::max<uint64_t>(n, 4096);
-  BH_HIP(hipMalloc(&ctx->cnt, want * 4));
-  BH_HIP(hipMemsetAsync(ctx->cnt, 0, want * 4, ctx->stream));
-  ctx->cnt_n = want;
-  return BH_OK;
+  size_t have = ctx->cnt_n * 4;
+  int rc = bh::grow_buffer(ctx, ctx->cnt, have, std::max<uint64_t>(n, 4096) * 4, true, "split-K tickets");
+  ctx->cnt_n = have / 4;
+  return rc;
 }
 
 // Number of K splits: enough blocks to cover the CUs twice, at least MIN_KT K tiles per split.
@@ -899,7 +883,7 @@ void load_tuning() {
 
 // Kernel choice for shapes the tuning table lacks. ring = false: no ring (LDS-DMA, packed
 // bank) config -- launch_conv's fallback when the bank or input is too large for it.
-choice_t heuristic(int op, const uint32_t *d, bool ring = true) {
+choice_t heuristic(int op, const uint32_t *d, bool ring = true, bool direct = true) {
   choice_t ch;
   if (op == 0) {
     ch.cfg = 0;
@@ -1073,6 +1057,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
     s = std::string("mfma32_conv_") + (k1 ? "1x1_" : "im2col_") + c.name + ((K % 4 == 0) ? "_avec" : "_ascalar");
   }
   if (c.streamk) return s + "_streamk";
+  if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
   uint32_t S = resolve_splits(c, ch, M, N, K, 256);
   if (S > 1) {
@@ -1134,7 +1119,8 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases, float *out, uint32_t B,
                 uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
-                uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot, const float *res) {
+                uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot, const float *res,
+                bool no_dc) {
   // out_ctot: channels of the tensor `out` points into (0: OC). Every conv epilogue addresses
   // image i of the output at i * OCOHW, so a conv can write its channel slab of a wider
   // tensor (a Concat's output) in place.
@@ -1166,6 +1152,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   const bool avec = (K % 4 == 0) && ((uintptr_t)filts % 16 == 0);
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
+  if (no_dc && cfgs(1)[ch.cfg].dc) ch = heuristic(1, d, true, false);
   if (cfgs(1)[ch.cfg].gv) {
     // few output columns: stream the bank in its reference layout; the window covering the
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
@@ -1196,6 +1183,12 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       p.a_bytes = kp * oc4 * 4;
       p.IC = IC;
       set_fd(IC, p.ic_m, p.ic_s);
+      if (cfgs(1)[ch.cfg].dc) {
+        const int rc = launch_dc(ctx, cfgs(1)[ch.cfg], p, B, KY, KX, sy, sx, packed != nullptr);
+        if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
+        return launch_conv(ctx, in, filts, packed ? packed : wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py,
+                           px, relu, out_ctot, res, true);
+      }
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
       const bool tab = ((p.K + bk - 1) / bk) * bk <= (uint32_t)TAB_MAX;  // K rows a block tabulates
       const int bld = k1 ? (IC % bk == 0 ? B_IM1X1S : B_IM1X1)

@@ -12,7 +12,8 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 enum { A_KVEC = 0, A_KSCALAR = 1, A_MVEC = 2, A_MSCALAR = 3 };
 enum { B_KVEC = 0, B_KSCALAR = 1, B_IM2COL = 2, B_IM1X1 = 3, B_IM1X1V = 4, B_IMT2 = 5, B_FC = 6, B_IMTAB = 7,
-       B_IMTAP = 8, B_IM1X1S = 9, NBLD = 10 };
+       B_IMTAP = 8, B_IM1X1S = 9, B_DIRECT = 10, NBLD = 11 };
+// B_DIRECT: direct-conv kernels (bh_direct.hip): the input strip staged whole per block
 // B_IM1X1S: ring kernels' 1x1 loader when K % BK == 0: the lane's pixel offset (VGPR, a miss
 // for dead stages) + each row's channel offset as the scalar soffset
 // B_IMTAP: ring kernels' im2col when IC % BK == 0: a K tile lies inside one filter tap, so a
@@ -264,6 +265,8 @@ struct cfg_t {
   int streamk = 0;    // persistent stream-K grid (srk_kernel): k[..][..][0] only
   int lds_bytes = 0;  // static LDS per block (stream-K grid sizing)
   int gv = 0;         // filter-streaming kernel (bh_gv.hip): grid (M / BM) x K chunks, BN >= N
+  int dc = 0;         // direct conv (bh_direct.hip): kernel dc_ky x dc_kx, stride dc_s, strip dc_rin x dc_wpm
+  int dc_ky = 0, dc_kx = 0, dc_s = 0, dc_wpm = 0, dc_rin = 0;
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and
@@ -271,6 +274,10 @@ struct cfg_t {
 std::vector<cfg_t> ring_cfgs(int op);
 // bh_gv.hip: filter-streaming configurations for convs with few output columns
 std::vector<cfg_t> gv_cfgs();
+// bh_direct.hip: direct-conv configurations for the few-channel stem layers
+std::vector<cfg_t> dc_cfgs();
+int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+              uint32_t sx, bool first);
 int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint32_t IC, uint32_t KYX, bool first,
                        bool last);
 int ensure_wpack(bh_ctx *ctx, size_t bytes);

@@ -934,16 +934,7 @@ int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint
 }
 
 int ensure_wpack(bh_ctx *ctx, size_t bytes) {
-  if (ctx->wpack_bytes >= bytes) return BH_OK;
-  if (ctx->wpack) {
-    BH_HIP(hipStreamSynchronize(ctx->stream));
-    BH_HIP(hipFree(ctx->wpack));
-    ctx->wpack = nullptr;
-    ctx->wpack_bytes = 0;
-  }
-  BH_HIP(hipMalloc(&ctx->wpack, bytes));
-  ctx->wpack_bytes = bytes;
-  return BH_OK;
+  return bh::grow_buffer(ctx, ctx->wpack, ctx->wpack_bytes, bytes, false, "filter-bank pack buffer");
 }
 
 }  // namespace bhk

@@ -39,6 +39,32 @@ int check_launch(const char *what) {
   return BH_OK;
 }
 
+int grow_buffer(bh_ctx *ctx, void *&buf, size_t &have, size_t want, bool zero, const char *what) {
+  if (have >= want) return BH_OK;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  BH_HIP(hipStreamIsCapturing(ctx->stream, &st));
+  if (st != hipStreamCaptureStatusNone)
+    return fail(BH_ERR, std::string(what) + ": the per-context workspace must grow (" + std::to_string(want) +
+                            " bytes) while the stream is being captured; run this op once eagerly before capturing");
+  if (buf) {
+    bool live_graph = false;
+    for (hipGraphExec_t g : ctx->graphs) live_graph |= g != nullptr;
+    if (live_graph) {
+      ctx->retired.push_back(buf);  // a captured graph may still replay this pointer
+    } else {
+      BH_HIP(hipStreamSynchronize(ctx->stream));
+      BH_HIP(hipFree(buf));
+    }
+    buf = nullptr;
+    have = 0;
+  }
+  const size_t sz = want + (want >> 2);
+  BH_HIP(hipMalloc(&buf, sz));
+  if (zero) BH_HIP(hipMemsetAsync(buf, 0, sz, ctx->stream));
+  have = sz;
+  return BH_OK;
+}
+
 int launch(bh_ctx *ctx, const void *kernel, dim3 grid, dim3 block, void **args, bool first, bool last,
            const char *what) {
   hipEvent_t b = first ? ctx->t_start : nullptr, e = last ? ctx->t_stop : nullptr;
@@ -98,12 +124,13 @@ int bh_init(int device, bh_ctx **out) {
 }
 
 int bh_destroy(bh_ctx *c) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
   for (hipGraphExec_t g : c->graphs)
     if (g) (void)hipGraphExecDestroy(g);
+  for (void *r : c->retired) (void)hipFree(r);
   if (c->ws) (void)hipFree(c->ws);
   if (c->wpack) (void)hipFree(c->wpack);
   if (c->stamps) (void)hipFree(c->stamps);
@@ -114,7 +141,7 @@ int bh_destroy(bh_ctx *c) {
 }
 
 int bh_plat_tag(bh_ctx *c, char *buf, size_t n) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
   // the marketing name comes from libdrm's amdgpu.ids; where that table is missing (some
   // launch environments) HIP reports a generic "AMD Radeon Graphics": gfx950 is MI355X
@@ -124,17 +151,16 @@ int bh_plat_tag(bh_ctx *c, char *buf, size_t n) {
 }
 
 int bh_get_stream(bh_ctx *c, void **s) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!s) return bh::fail(BH_ERR, "null out");
   *s = (void *)c->stream;
   return BH_OK;
 }
 
 int bh_alloc(bh_ctx *c, size_t bytes, void **p) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!p) return bh::fail(BH_ERR, "null out");
   *p = nullptr;
-  BH_HIP(hipSetDevice(c->device));
   void *d = nullptr;
   BH_HIP(hipMalloc(&d, bytes ? bytes : 16));
   hipError_t e = hipMemsetAsync(d, 0, bytes ? bytes : 16, c->stream);
@@ -148,21 +174,20 @@ int bh_alloc(bh_ctx *c, size_t bytes, void **p) {
 }
 
 int bh_free(bh_ctx *c, void *p) {
-  BH_CHECK_CTX(c);
-  BH_HIP(hipSetDevice(c->device));
+  BH_ENTER(c);
   BH_HIP(hipStreamSynchronize(c->stream));
   BH_HIP(hipFree(p));
   return BH_OK;
 }
 
 int bh_memset0(bh_ctx *c, void *p, size_t bytes) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   BH_HIP(hipMemsetAsync(p, 0, bytes, c->stream));
   return BH_OK;
 }
 
 int bh_h2d(bh_ctx *c, void *d, const void *h, size_t bytes) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   // synchronous w.r.t. the host buffer (caller may free it on return)
   BH_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
   BH_HIP(hipStreamSynchronize(c->stream));
@@ -170,20 +195,20 @@ int bh_h2d(bh_ctx *c, void *d, const void *h, size_t bytes) {
 }
 
 int bh_d2h(bh_ctx *c, void *h, const void *d, size_t bytes) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   BH_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
   BH_HIP(hipStreamSynchronize(c->stream));
   return BH_OK;
 }
 
 int bh_sync(bh_ctx *c) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   BH_HIP(hipStreamSynchronize(c->stream));
   return BH_OK;
 }
 
 int bh_event_record(bh_ctx *c, int *id) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!id) return bh::fail(BH_ERR, "null out");
   if (c->events_used == (int)c->events.size()) {
     hipEvent_t ev;
@@ -196,7 +221,7 @@ int bh_event_record(bh_ctx *c, int *id) {
 }
 
 int bh_time_next_call(bh_ctx *c, int *begin_id, int *end_id) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!begin_id || !end_id) return bh::fail(BH_ERR, "null out");
   for (int k = 0; k < 2; ++k)
     if (c->events_used + k >= (int)c->events.size()) {
@@ -212,7 +237,7 @@ int bh_time_next_call(bh_ctx *c, int *begin_id, int *end_id) {
 }
 
 int bh_elapsed_ms(bh_ctx *c, int b, int e, float *ms) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!ms) return bh::fail(BH_ERR, "null out");
   if (b < 0 || e < 0 || b >= c->events_used || e >= c->events_used) return bh::fail(BH_ERR, "bad event id");
   BH_HIP(hipEventSynchronize(c->events[e]));
@@ -221,19 +246,19 @@ int bh_elapsed_ms(bh_ctx *c, int b, int e, float *ms) {
 }
 
 int bh_events_reset(bh_ctx *c) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   c->events_used = 0;
   return BH_OK;
 }
 
 int bh_gen_data(bh_ctx *c, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!dst || !dims) return bh::fail(BH_ERR, "null argument");
   return bh::launch_gen_data(c, kind, dst, dims, mode, vi);
 }
 
 int bh_sgemm_kmajor(bh_ctx *c, const float *a, const float *b, float *cc, uint32_t M, uint32_t N, uint32_t K) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!a || !b || !cc) return bh::fail(BH_ERR, "null tensor");
   if (!M || !N || !K) return bh::fail(BH_UNSUP, "sgemm: zero-sized dimension");
   return bh::launch_sgemm(c, a, b, cc, M, N, K);
@@ -242,7 +267,7 @@ int bh_sgemm_kmajor(bh_ctx *c, const float *a, const float *b, float *cc, uint32
 int bh_conv2d_fwd_nchw_pk(bh_ctx *c, const float *in, const float *filts, const float *packed, const float *biases,
                           float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                           uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
     return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
@@ -253,7 +278,7 @@ int bh_conv2d_fwd_nchw_pk(bh_ctx *c, const float *in, const float *filts, const 
 int bh_conv2d_fwd_nchw_res(bh_ctx *c, const float *in, const float *filts, const float *packed, const float *biases,
                            const float *res, float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC,
                            uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
     return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
@@ -265,7 +290,7 @@ int bh_conv2d_fwd_nchw_slab(bh_ctx *c, const float *in, const float *filts, cons
                             const float *biases, float *out, uint32_t out_chans_total, uint32_t out_chan_ofs,
                             uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
                             uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
     return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
@@ -290,7 +315,7 @@ int bh_pool_out_size(uint32_t in, uint32_t k, uint32_t stride, uint32_t pad) {
 int bh_pool_fwd_nchw(bh_ctx *c, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C, uint32_t H,
                      uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px,
                      int avg) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !C || !H || !W || !KY || !KX || !sy || !sx) return bh::fail(BH_UNSUP, "pool: zero-sized dimension");
   if (py >= KY || px >= KX) return bh::fail(BH_UNSUP, "pool: padding must be smaller than the window");
@@ -299,21 +324,21 @@ int bh_pool_fwd_nchw(bh_ctx *c, const float *in, float *out, float *out_in_yx, u
 
 int bh_lrn_fwd_nchw(bh_ctx *c, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
                     uint32_t W, uint32_t local_size, float alpha, float beta, float k) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !out) return bh::fail(BH_ERR, "null tensor");
   if (!B || !C || !H || !W) return bh::fail(BH_UNSUP, "lrn: zero-sized dimension");
   return bh::launch_lrn(c, in, out, out_scale_base, B, C, H, W, local_size, alpha, beta, k);
 }
 
 int bh_relu_inplace(bh_ctx *c, float *x, uint64_t n) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!x) return bh::fail(BH_ERR, "null tensor");
   if (!n) return BH_OK;
   return bh::launch_relu(c, x, n);
 }
 
 int bh_softmax_chans(bh_ctx *c, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !prob) return bh::fail(BH_ERR, "null tensor");
   if (!B || !C || !H || !W) return bh::fail(BH_UNSUP, "softmax: zero-sized dimension");
   return bh::launch_softmax(c, in, prob, B, C, H, W);
@@ -321,20 +346,20 @@ int bh_softmax_chans(bh_ctx *c, const float *in, float *prob, uint32_t B, uint32
 
 int bh_chan_copy(bh_ctx *c, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
                  uint32_t out_c, uint32_t oc0, uint32_t nc) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !out) return bh::fail(BH_ERR, "null tensor");
   return bh::launch_chan_copy(c, in, out, B, HW, in_c, ic0, out_c, oc0, nc);
 }
 
 int bh_chan_affine(bh_ctx *c, const float *in, float *out, const float *scale, const float *shift, uint32_t B,
                    uint32_t C, uint32_t HW, int relu) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!in || !out || !scale || !shift) return bh::fail(BH_ERR, "null tensor");
   return bh::launch_chan_affine(c, in, out, scale, shift, B, C, HW, relu ? 1 : 0);
 }
 
 int bh_eltwise(bh_ctx *c, const float *a, const float *b, float *out, uint64_t n, int op, int relu) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!a || !b || !out) return bh::fail(BH_ERR, "null tensor");
   if (!n) return BH_OK;
   return bh::launch_eltwise(c, a, b, out, n, op, relu ? 1 : 0);
@@ -346,7 +371,7 @@ size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32
 
 int bh_conv_filts_pack(bh_ctx *c, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                        uint32_t KX) {
-  BH_CHECK_CTX(c);
+  BH_ENTER_CALL(c);
   if (!filts || !packed) return bh::fail(BH_ERR, "null tensor");
   if (!OC || !IC || !KY || !KX) return bh::fail(BH_UNSUP, "conv_filts_pack: zero-sized dimension");
   return bh::launch_conv_filts_pack(c, filts, packed, OC, IC, KY, KX);
@@ -363,7 +388,7 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
 }
 
 int bh_stamp(bh_ctx *c, int slot) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (slot < 0 || slot >= STAMP_SLOTS) return bh::fail(BH_ERR, "stamp slot out of range");
   unsigned long long *t = (unsigned long long *)c->stamps;
   void *args[] = {&t, &slot};
@@ -372,7 +397,7 @@ int bh_stamp(bh_ctx *c, int slot) {
 }
 
 int bh_spin(bh_ctx *c, int us) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (us < 1 || us > 100000) return bh::fail(BH_ERR, "bh_spin: us out of range 1..100000");
   unsigned long long ticks = (unsigned long long)us * (unsigned long long)(c->stamp_hz / 1e6);
   void *args[] = {&ticks};
@@ -381,7 +406,7 @@ int bh_spin(bh_ctx *c, int us) {
 }
 
 int bh_stamps_read(bh_ctx *c, int first, int n, double *us) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!us || first < 0 || n < 0 || first + n > STAMP_SLOTS) return bh::fail(BH_ERR, "bad stamp range");
   std::vector<unsigned long long> t(n);
   BH_HIP(hipMemcpyAsync(t.data(), (unsigned long long *)c->stamps + first, n * sizeof(unsigned long long),
@@ -392,13 +417,13 @@ int bh_stamps_read(bh_ctx *c, int first, int n, double *us) {
 }
 
 int bh_capture_begin(bh_ctx *c) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   BH_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   return BH_OK;
 }
 
 int bh_capture_end(bh_ctx *c, int *graph_id) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (!graph_id) return bh::fail(BH_ERR, "null out");
   hipGraph_t g = nullptr;
   BH_HIP(hipStreamEndCapture(c->stream, &g));
@@ -412,14 +437,14 @@ int bh_capture_end(bh_ctx *c, int *graph_id) {
 }
 
 int bh_graph_launch(bh_ctx *c, int graph_id) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (graph_id < 0 || graph_id >= (int)c->graphs.size() || !c->graphs[graph_id]) return bh::fail(BH_ERR, "bad graph id");
   BH_HIP(hipGraphLaunch(c->graphs[graph_id], c->stream));
   return BH_OK;
 }
 
 int bh_graph_destroy(bh_ctx *c, int graph_id) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   if (graph_id < 0 || graph_id >= (int)c->graphs.size() || !c->graphs[graph_id]) return bh::fail(BH_ERR, "bad graph id");
   BH_HIP(hipStreamSynchronize(c->stream));
   BH_HIP(hipGraphExecDestroy(c->graphs[graph_id]));
@@ -428,7 +453,7 @@ int bh_graph_destroy(bh_ctx *c, int graph_id) {
 }
 
 int bh_tune_set(bh_ctx *c, int op, int cfg_index, int splits) {
-  BH_CHECK_CTX(c);
+  BH_ENTER(c);
   return bh::tune_set(c, op, cfg_index, splits);
 }
 
