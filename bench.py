@@ -19,11 +19,18 @@ device with the reference's gen_data mode 5 before the timed region).
   cpu_baseline= the oracle's fp32 OpenMP CPU implementation (kind "port") on a
                 bounded sample, rank 0 at N=1 only
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-ops are independent so there is no data-path collective; every
-rank runs one full copy of the op list on its own GPU (weak scaling), a gloo
-barrier brackets the timed region and the max wall time over ranks is used.
---strong instead shards ONE op list over the ranks (greedy LPT on roofline time).
+Workload: sgemm-ops-full + conv-ops-1-5-20 (the metric's two lists, BASELINE configs C2/C3)
++ op_sigs_full (C5) -- the same fixed list at every N, so per-N values compare directly.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): ops are
+independent (src/rtc_prof.cc:232-360), so the list is SHARDED over the ranks
+with no data-path collective: greedy LPT on roofline time (boda_hip/shard.py, the algorithm of
+boda_hip_ops_prof --shard=k/n), SGEMMs bigger than half a rank's share first cut into column
+panels (independent M x n_j x K sub-ops). Each rank runs its units on its own GPU; a gloo
+barrier brackets the timed region and the max wall time over ranks is used ("scaling":
+"strong": the total work is fixed). The line carries the predicted LPT imbalance (max rank
+roofline load / mean) and the measured one (max rank wall time / mean). More ranks than GPUs
+is refused unless --rehearsal (then "shared_device": true).
 """
 import argparse
 import json
@@ -37,7 +44,7 @@ sys.path.insert(0, ROOT)
 
 import boda_hip  # noqa: E402
 from boda_hip import ops, runner  # noqa: E402
-from boda_hip.shard import Dist, lpt_partition  # noqa: E402
+from boda_hip.shard import Dist, imbalance, lpt_partition, plan_units  # noqa: E402
 
 OPS_DIR = os.path.join(ROOT, "tests", "golden", "ops")
 SETS = {
@@ -47,7 +54,7 @@ SETS = {
     "conv": "conv-ops-1-5-20-nin-alex-gn.txt",
     "op-sigs": "op_sigs_full.txt",
 }
-DEFAULT_SETS = ["sgemm-full", "conv"]
+DEFAULT_SETS = ["sgemm-full", "conv", "op-sigs"]
 
 
 def load_sets(names):
@@ -58,6 +65,15 @@ def load_sets(names):
             shapes.append(ops.shape_of(op))
             tags.append(n)
     return shapes, tags
+
+
+def shard_units(shapes, tags, world, rank):
+    """This rank's units of the sharded sweep: (all units, my units, predicted LPT imbalance)."""
+    costs = [runner.roofline_secs(s) for s in shapes]
+    units = plan_units(shapes, costs, world)
+    parts = lpt_partition([u[2] for u in units], world)
+    pred = imbalance([sum(units[i][2] for i in p) for p in parts])
+    return units, [units[i] for i in parts[rank]], pred
 
 
 def cpu_baseline(budget_s):
@@ -96,10 +112,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", default=",".join(DEFAULT_SETS))
-    ap.add_argument("--strong", action="store_true", help="shard one op list over the ranks (LPT)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than GPUs (ranks share devices; the line says shared_device)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--per-op", default="", help="write per-op event times (JSON) to this path")
+    ap.add_argument("--per-op", default="", help="write per-unit times (JSON, all ranks) to this path")
     ap.add_argument("--eager", action="store_true", help="launch op by op from Python instead of hipGraph replay")
     ap.add_argument("--op-timing", choices=["graph", "events"], default="graph",
                     help="per-op time: amortized over a replayed graph of back-to-back calls (default), or HIP "
@@ -108,26 +125,27 @@ def main():
 
     dd = Dist()
     if dd.world != args.gpus:
-        if args.gpus > 1:
-            sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
+        sys.exit("--gpus %d needs torch.distributed.run with %d ranks (got world size %d)" % (args.gpus, args.gpus,
+                                                                                        dd.world))
+    ndev = boda_hip.device_count()
+    shared = dd.max(1.0 if dd.local_rank >= ndev else 0.0) > 0  # some rank has no GPU of its own
+    if shared and not args.rehearsal:
+        sys.exit("rank %d: local rank %d but only %d GPU(s); pass --rehearsal to let ranks share a device"
+                 % (dd.rank, dd.local_rank, ndev))
     set_names = [s for s in args.sets.split(",") if s]
     shapes, tags = load_sets(set_names)
-    if args.strong and dd.world > 1:
-        mine = lpt_partition([runner.roofline_secs(s) for s in shapes], dd.world)[dd.rank]
-    else:
-        mine = list(range(len(shapes)))
-    my_shapes = [shapes[i] for i in mine]
-    my_tags = [tags[i] for i in mine]
+    units, mine, pred_imb = shard_units(shapes, tags, dd.world, dd.rank)
+    my_shapes = [u[1] for u in mine]
+    my_tags = [tags[u[0]] for u in mine]
 
-    # one GPU per rank; ranks beyond the node's GPU count share (rehearsal on a 1-GPU box)
-    dev = boda_hip.Device(dd.local_rank % max(1, boda_hip.device_count()))
+    dev = boda_hip.Device(dd.local_rank % max(1, ndev))
     wl = runner.Workload(dev, my_shapes, mode=5, tags=my_tags)
     for _ in range(args.warmup):
         wl.step()
     dev.sync()
 
-    # Timed region: K steps, each a captured hipGraph of the whole op sweep, replayed
-    # back to back (--eager: launched op by op from Python instead).
+    # Timed region: K steps, each a captured hipGraph of this rank's sweep, replayed back to
+    # back (--eager: launched op by op from Python instead).
     nop = len(my_shapes)
     graphs = [] if args.eager else [wl.capture_step() for _ in range(args.steps)]
     dd.barrier()
@@ -143,6 +161,7 @@ def main():
     t1 = time.perf_counter()
     dd.barrier()
     elapsed = dd.max(t1 - t0)
+    rank_times = dd.gather_obj(t1 - t0)
 
     # Per-op GPU time (the reference's per-op convention, src/rtc_prof.cc:104-124): K more
     # steps, each op timed by HIP events recorded on its own first/last kernel dispatch.
@@ -168,28 +187,36 @@ def main():
     total_flops = dd.sum(my_flops) * args.steps
     value = total_flops / elapsed / 1e9
 
-    per_set = {}
-    for n in set_names:
-        idx = [i for i, t in enumerate(my_tags) if t == n]
-        if not idx:
-            continue
-        f = sum(my_shapes[i].flops() for i in idx)
-        t = sum(ktime[i] for i in idx)
-        rt = sum(runner.roofline_secs(my_shapes[i]) for i in idx)
-        per_set[n] = {"ops": len(idx), "gflop": round(f / 1e9, 3), "sum_kernel_ms": round(t * 1e3, 4),
-                      "gflops": round(f / t / 1e9, 2), "roofline_frac": round(rt / t, 4),
-                      "roofline_ms": round(rt * 1e3, 4)}
-
-    # dominant kernel: the variant with the most event time
-    by_var = {}
+    # every rank's per-unit records, gathered on rank 0 (per-set sums and the dominant kernel are
+    # over the whole job)
+    recs = []
     for i, s in enumerate(my_shapes):
         kind = 0 if isinstance(s, ops.SgemmShape) else 1
         dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
-        v = boda_hip.variant_name(kind, dims)
-        d = by_var.setdefault(v, {"t": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
-        d["t"] += ktime[i]
-        d["flops"] += s.flops()
-        d["bytes"] += s.bytes()
+        recs.append({"tag": my_tags[i], "op": mine[i][0], "dims": dims, "variant": boda_hip.variant_name(kind, dims),
+                     "flops": s.flops(), "bytes": s.bytes(), "kernel_s": ktime[i], "event_s": ev_time[i],
+                     "roof_s": runner.roofline_secs(s), "bound": runner.bound_of(s), "rank": dd.rank})
+    recs = [r for part in dd.gather_obj(recs) for r in part]
+
+    per_set = {}
+    for n in set_names:
+        rs = [r for r in recs if r["tag"] == n]
+        if not rs:
+            continue
+        f = sum(r["flops"] for r in rs)
+        t = sum(r["kernel_s"] for r in rs)
+        rt = sum(r["roof_s"] for r in rs)
+        per_set[n] = {"ops": len({r["op"] for r in rs}), "gflop": round(f / 1e9, 3), "sum_kernel_ms": round(t * 1e3, 4),
+                      "gflops": round(f / t / 1e9, 2), "roofline_frac": round(rt / t, 4),
+                      "roofline_ms": round(rt * 1e3, 4)}
+
+    # dominant kernel: the variant with the most time over the whole job
+    by_var = {}
+    for r in recs:
+        d = by_var.setdefault(r["variant"], {"t": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
+        d["t"] += r["kernel_s"]
+        d["flops"] += r["flops"]
+        d["bytes"] += r["bytes"]
         d["n"] += 1
     dom = max(by_var, key=lambda v: by_var[v]["t"])
     dv = by_var[dom]
@@ -214,18 +241,17 @@ def main():
 
     if args.per_op and dd.rank == 0:
         with open(args.per_op, "w") as f:
-            json.dump([{"tag": my_tags[i], "dims": (my_shapes[i].as_dims() if isinstance(my_shapes[i], ops.ConvShape)
-                                                   else [my_shapes[i].M, my_shapes[i].N, my_shapes[i].K]),
-                        "kernel_ms": ktime[i] * 1e3, "event_ms": ev_time[i] * 1e3, "gflops": my_shapes[i].flops() / ktime[i] / 1e9,
-                        "roofline_frac": runner.roofline_secs(my_shapes[i]) / ktime[i],
-                        "bound": runner.bound_of(my_shapes[i])} for i in range(len(my_shapes))], f, indent=0)
+            json.dump([dict(r, kernel_ms=r["kernel_s"] * 1e3, event_ms=r["event_s"] * 1e3,
+                            gflops=r["flops"] / r["kernel_s"] / 1e9, roofline_frac=r["roof_s"] / r["kernel_s"])
+                       for r in recs], f, indent=0)
 
     if dd.rank == 0:
+        n_split = len({u[0] for u in units if u[1] != shapes[u[0]]})
         line = {
             "metric": "per-op GFLOPS and % fp32 roofline on sgemm-ops-full + conv-ops (AlexNet/NiN/GoogLeNet)",
             "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": dd.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if (args.strong and dd.world > 1) else "weak", "vs_baseline": None,
+            "scaling": "strong", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (reference gen_data mode 5, generated on device)",
             "config": {"workload": " + ".join(SETS[n] for n in set_names) + " (one main-kernel launch per op per step)",
                        "launch": "eager" if args.eager else "hipGraph replay of each step",
@@ -234,8 +260,12 @@ def main():
                                      if args.op_timing == "graph" else
                                      "HIP events on each op's first/last kernel dispatch (hipExtLaunchKernel), "
                                      "K extra eager steps after the timed region"),
-                       "ops_per_gpu": len(my_shapes), "gflop_per_step_per_gpu": round(my_flops / 1e9, 3),
-                       "parallelism": ("op-shard" if args.strong else "op-replica") + "%d" % dd.world,
+                       "ops": len(shapes), "units": len(units), "ops_cut_into_panels": n_split,
+                       "gflop_per_step": round(sum(s.flops() for s in shapes) / 1e9, 3),
+                       "parallelism": "op-shard%d (LPT, no collective)" % dd.world,
+                       "lpt_imbalance_predicted": round(pred_imb, 4),
+                       "lpt_imbalance_measured": round(imbalance(rank_times), 4),
+                       "shared_device": shared,
                        "plat": dev.plat_tag()},
             "per_set": per_set,
             "roofline": roof,

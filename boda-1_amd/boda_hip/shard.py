@@ -7,6 +7,8 @@ control plane (barrier, max / sum of timings) over gloo on the host.
 
   lpt_partition  greedy longest-processing-time split of an op list by cost
                  (the same algorithm as boda_hip_ops_prof --shard=k/n)
+  plan_units     the units a sharded sweep deals out: every op, with the SGEMMs too big
+                 for one rank's share cut into column panels (independent sub-ops)
   Dist           rank / world from the torchrun environment, gloo barrier and
                  max / sum reductions of host floats
 """
@@ -23,6 +25,45 @@ def lpt_partition(costs, n):
         bins[j].append(i)
         load[j] += costs[i]
     return [sorted(b) for b in bins]
+
+
+def plan_units(shapes, costs, n, panel_align=128, max_frac=0.5):
+    """Units of work for an n-way sharded sweep: (op index, shape, cost) triples.
+
+    Ops are independent (src/rtc_prof.cc:232-360), so LPT over whole ops is enough unless one
+    op outweighs a rank's share: sgemm-ops-full's 12288^3 alone is ~40 % of the list, which
+    would cap 8-way strong scaling near 2.5x. An SGEMM c[M][N] = sum_k a[k][M] b[k][N] with
+    cost > max_frac * total / n is cut into P column panels c[:, Nj] = a^T b[:, Nj] -- each an
+    independent M x nj x K SGEMM (no exchange: a panel is its own output slab) -- of widths that
+    are multiples of panel_align, P the least count that brings every panel under the bound.
+    Other ops (convolutions: at most ~0.2 % of this list each) stay whole. At n == 1 nothing is
+    cut. Returns units in op order (panels of an op consecutive)."""
+    from .ops import SgemmShape
+    total = float(sum(costs))
+    bound = max_frac * total / n if n > 1 else float("inf")
+    units = []
+    for i, (s, c) in enumerate(zip(shapes, costs)):
+        if not isinstance(s, SgemmShape) or c <= bound:
+            units.append((i, s, c))
+            continue
+        P = int(-(-c // bound))
+        cols = -(-s.N // panel_align)  # panel_align-wide column groups
+        P = max(1, min(P, cols))
+        base, extra = divmod(cols, P)
+        n0 = 0
+        for j in range(P):
+            w = min((base + (1 if j < extra else 0)) * panel_align, s.N - n0)
+            sub = SgemmShape(s.M, w, s.K)
+            units.append((i, sub, c * w / s.N))
+            n0 += w
+        assert n0 == s.N
+    return units
+
+
+def imbalance(loads):
+    """max / mean of per-rank loads (1.0 = perfectly balanced)."""
+    m = sum(loads) / len(loads)
+    return max(loads) / m if m > 0 else 1.0
 
 
 class Dist:

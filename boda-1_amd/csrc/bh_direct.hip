@@ -187,6 +187,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
   }
   const bool vec = p.cvec != 0;
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  constexpr int NSTW = TM * (32 / ER) * (CPP / 256);  // float4 stores per wave per tile
+  bool after_epi = false;
   int slot = 0;
   uint32_t g = 0;
   // outer loop over the block's tiles, inner over a tile's input channels (nested: the
@@ -210,16 +214,21 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
         for (int r = 0; r < 16; ++r) acc[t][tn][r] = 0.0f;
     int cslot = 0;
     for (uint32_t ic = 0; ic < p.IC; ++ic, ++g) {
-      vm_wait<(D - 2) * LW>();
+      // the first stage of a tile after an epilogue: that epilogue's stores (younger than this
+      // stage's DMAs) may stay in flight
+      if (after_epi && ic == 0) vm_wait<((D - 2) * LW + NSTW < 63 ? (D - 2) * LW + NSTW : 63)>();
+      else vm_wait<(D - 2) * LW>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage g landed for all waves; all done reading g-1
       asm volatile("" ::: "memory");
       if (i == 0 && ic == 0) KT(1);
+      if (i == 1 && ic == 0) KT(5);
       compute(slot, slot == 0 ? D - 1 : slot - 1, g + D - 1);  // + stage g+D-1 into slot (g-1) % D
       cslot = slot;
       slot = slot == D - 1 ? 0 : slot + 1;
     }
     if (i == 0) KT(2);
+    if (i == 1) KT(6);
 
     // ---- epilogue through LDS, in the slot of the stage just consumed (no DMA targets it
     // before the next stage's compute): ER rows of every MFMA tile at a time are written by
@@ -228,7 +237,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     // dword stores (the store issue bounds such an epilogue: cdna_hip_programming.md T21)
     float *const Cs = smem + cslot * SLOT;
     const float *const Lb = smem + cslot * SLOT + WREG + SREG;
-    const size_t obase = (size_t)img * p.OCOHW;
+    const uint32_t obase = img * p.OCOHW;
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
 #pragma unroll
@@ -246,34 +255,40 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        // buffer stores with misses for dead lanes (no branches): every wave issues exactly
+        // NSTW store instructions per tile on the float4 path, which the next tile's first
+        // stage wait leaves in flight
 #pragma unroll
         for (int j = 0; j < CPP / 256; ++j) {
           const int c = tid + 256 * j, row = c / (NPX / 4), col = 4 * (c % (NPX / 4));
           const int trow = 32 * t + h * ER + row;
           const uint32_t m = oc0 + (uint32_t)trow, px = p0 + (uint32_t)col;
-          if (m < p.M && px < p.OHW) {
-            f32x4v v = *(const f32x4v *)&Cs[row * NPX + col];
-            const float bb = Lb[trow];
-            const size_t o = obase + (size_t)m * p.OHW + px;
-            if (vec && px + 4 <= p.OHW) {
-              v += bb;
-              if (p.res) v += *(const f32x4v *)&p.res[o];
+          const bool live = (m < p.M) & (px < p.OHW);
+          f32x4v v = *(const f32x4v *)&Cs[row * NPX + col];
+          const float bb = Lb[trow];
+          const uint32_t o = obase + m * p.OHW + px;  // (host: the output is < 2 GiB)
+          if (vec) {
+            v += bb;
+            if (p.res) v += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsr, oob_unless(live, o * 4u), 0, 0));
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = (p.relu && v[q] < 0.0f) ? 0.0f : v[q];
-              *(f32x4v *)&p.c[o] = v;
-            } else {
+            for (int q = 0; q < 4; ++q) v[q] = (p.relu && v[q] < 0.0f) ? 0.0f : v[q];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                   rso, oob_unless(live, o * 4u), 0, 0);
+          } else {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                if (px + q >= p.OHW) break;
-                float x = v[q] + bb;
-                if (p.res) x += p.res[o + q];
-                p.c[o + q] = (p.relu && x < 0.0f) ? 0.0f : x;
-              }
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t oq = oob_unless(live & (px + q < p.OHW), (o + q) * 4u);
+              float x = v[q] + bb;
+              if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, oq, 0, 0));
+              x = (p.relu && x < 0.0f) ? 0.0f : x;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, oq, 0, 0);
             }
           }
         }
       }
     }
+    after_epi = true;
+    if (i == 0) KT(3);
   }
   vm_wait<0>();
 #ifdef BH_KTRACE
@@ -299,11 +314,11 @@ cfg_t dc_cfg(const char *name) {
 std::vector<cfg_t> dc_cfgs() {
   return {
       // GoogLeNet conv1 (3 x 224^2 -> 64, 7x7 s2 p3); 96 channels: the op_sigs 7x7 s2 stem
-      dc_cfg<7, 7, 2, 232, 13, 2, 2, 2>("dc7s2x64d2"),
-      dc_cfg<7, 7, 2, 232, 13, 2, 2, 3>("dc7s2x64d3"),
-      dc_cfg<7, 7, 2, 232, 13, 1, 2, 3>("dc7s2x32d3"),
-      dc_cfg<7, 7, 2, 232, 13, 3, 2, 2>("dc7s2x96d2"),
-      dc_cfg<7, 7, 2, 232, 11, 2, 1, 2>("dc7s2x64n128d2"),
+      dc_cfg<7, 7, 2, 236, 13, 2, 2, 2>("dc7s2x64d2"),
+      dc_cfg<7, 7, 2, 236, 13, 2, 2, 3>("dc7s2x64d3"),
+      dc_cfg<7, 7, 2, 236, 13, 1, 2, 3>("dc7s2x32d3"),
+      dc_cfg<7, 7, 2, 236, 13, 3, 2, 2>("dc7s2x96d2"),
+      dc_cfg<7, 7, 2, 236, 11, 2, 1, 2>("dc7s2x64n128d2"),
       // AlexNet conv1 (3 x 227^2 / 224^2 -> 96, 11x11 s4)
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2>("dc11s4x96d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2>("dc11s4x32d2"),
@@ -331,6 +346,9 @@ int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY,
     if ((b / OW - a / OW) * sy + KY > (uint32_t)c.dc_rin)
       return bh::fail(BH_UNSUP, std::string("conv: pixel tile spans too many input rows for ") + c.name);
   }
+  const uint64_t out_bytes = (uint64_t)B * p.OCOHW * 4;
+  if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the direct kernel");
+  p.c_bytes = (uint32_t)out_bytes;
   const uint32_t octiles = (p.M + c.BM - 1) / c.BM;
   const uint64_t ntile = (uint64_t)B * tiles * octiles;
   if (ntile >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many tiles");

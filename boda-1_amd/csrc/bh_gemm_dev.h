@@ -45,6 +45,7 @@ struct GemmArgs {
   uint32_t tbm, tbn;          // tile shape (for the split-K combine)
   uint32_t ks;                // K extent of one split (multiple of BK)
   uint32_t a_bytes, b_bytes;  // buffer extents in bytes (reads beyond come back 0)
+  uint32_t c_bytes;           // output extent (direct conv: buffer stores; beyond = dropped)
   uint32_t tiles_m, tiles_n;
   int relu;
   int cvec;  // dense C rows can take TN-wide vector stores

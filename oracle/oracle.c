@@ -199,6 +199,35 @@ ORC_API void orc_conv_ref(const float *in, const float *filts, const float *bias
   }
 }
 
+/* The same sum for selected outputs only (flat NCHW output indices idx[0..n-1]), for shapes
+ * too large for a full double-accumulated reference in a test's time budget. */
+ORC_API void orc_conv_ref_at(const float *in, const float *filts, const float *biases, const uint64_t *idx,
+                             uint64_t n, float *vals, uint32_t B, uint32_t IC, uint32_t H, uint32_t W,
+                             uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py,
+                             uint32_t px, int relu) {
+  uint32_t OH = orc_conv_out_sz(H, py, KY, sy), OW = orc_conv_out_sz(W, px, KX, sx);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t e = idx[i];
+    uint32_t ox = (uint32_t)(e % OW), oy = (uint32_t)((e / OW) % OH);
+    uint32_t oc = (uint32_t)((e / ((uint64_t)OW * OH)) % OC), b = (uint32_t)(e / ((uint64_t)OW * OH * OC));
+    double acc = biases ? (double)biases[oc] : 0.0;
+    for (uint32_t ic = 0; ic < IC; ++ic)
+      for (uint32_t ky = 0; ky < KY; ++ky) {
+        int64_t iy = (int64_t)oy * sy + ky - py;
+        if (iy < 0 || iy >= (int64_t)H) continue;
+        for (uint32_t kx = 0; kx < KX; ++kx) {
+          int64_t ix = (int64_t)ox * sx + kx - px;
+          if (ix < 0 || ix >= (int64_t)W) continue;
+          acc += (double)in[(((size_t)b * IC + ic) * H + iy) * W + ix] *
+                 (double)filts[(((size_t)oc * IC + ic) * KY + ky) * KX + kx];
+        }
+      }
+    float v = (float)acc;
+    vals[i] = (relu && v < 0.0f) ? 0.0f : v;
+  }
+}
+
 /* ------------------------------------------------------------------------- */
 /* CPU baseline (fp32, OpenMP, blocked) -- timed by bench.py's cpu_baseline   */
 /* ------------------------------------------------------------------------- */

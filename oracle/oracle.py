@@ -38,6 +38,7 @@ def _lib():
         L.orc_sgemm_fast.argtypes = [vp, vp, vp, u32, u32, u32]
         L.orc_conv_ref.argtypes = [vp, vp, vp, vp] + [u32] * 11 + [ctypes.c_int]
         L.orc_conv_fast.argtypes = [vp, vp, vp, vp] + [u32] * 11 + [ctypes.c_int]
+        L.orc_conv_ref_at.argtypes = [vp, vp, vp, vp, u64, vp] + [u32] * 11 + [ctypes.c_int]
         L.orc_digest_plan.argtypes = [u64, vp, ctypes.c_int, u64, vp, ctypes.c_int]
         L.orc_digest_plan.restype = ctypes.c_int
         L.orc_digest.argtypes = [vp, u64, vp, ctypes.c_int, u64, f32p, f32p, vp, ctypes.c_int]
@@ -91,6 +92,15 @@ def conv_ref(inp, filts, biases, s, relu=1, fast=False):
     f(_p(inp), _p(filts), _p(biases) if biases is not None else None, _p(out),
       s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu))
     return out
+
+
+def conv_ref_at(inp, filts, biases, s, idx, relu=1):
+    """Double-accumulated outputs at the flat NCHW output indices idx (sampled checks of big shapes)."""
+    idx = np.ascontiguousarray(idx, np.uint64)
+    vals = np.empty(idx.size, np.float32)
+    _lib().orc_conv_ref_at(_p(inp), _p(filts), _p(biases) if biases is not None else None, _p(idx), idx.size,
+                           _p(vals), s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, int(relu))
+    return vals
 
 
 def set_threads(n):

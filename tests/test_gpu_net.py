@@ -51,6 +51,22 @@ def test_net_forward(net, tmp_path):
     assert rl2 <= 1e-4 and nm <= 1e-3, (net, nm, rl2)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("net", ["resnet-50", "vgg_19"])
+def test_net_forward_batch20(net, tmp_path):
+    """BASELINE config C4 at its batch: ResNet-50 / VGG-19 forward at batch 20 (BatchNorm / Scale
+    folding, residual epilogues and every b20 tuning-table route on) against the CPU net oracle --
+    the role of the reference's test_compute net comparison (src/test_compute.cc:216-276)."""
+    plan, x, got, _ = run_net(net, 20, tmp_path)
+    d0 = plan["inputs"][0]["dims"]
+    assert d0[0] == 20
+    np.testing.assert_array_equal(x, onet.det_hash_rand_vec(int(np.prod(d0)), onet.IN_SEED))
+    ref = onet.forward(plan, x.reshape(d0))[plan["out_node"]].reshape(-1)
+    nm, rl2, _ = orc.normalized_errors(ref, got)
+    print(net, "b20 out", plan["out_node"], "nm %.2e rl2 %.2e" % (nm, rl2))
+    assert rl2 <= 1e-4 and nm <= 1e-3, (net, nm, rl2)
+
+
 def test_net_unpacked_bank_same_bits(tmp_path):
     """--no-pack (filter banks transformed inside every conv call) gives the same output bits."""
     a = tmp_path / "a"

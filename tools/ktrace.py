@@ -35,13 +35,13 @@ def one(dev, wl, reps):
         marks = us[1:1 + NSLOT]
         post = us[-1]
         pts = {}
-        for k in range(5):
+        for k in range(8):
             v = [marks[b * 8 + k] for b in range(NSLOT // 8) if 0 < marks[b * 8 + k] <= post]
             if v:
                 pts[k] = v
         # per-block phase durations: prologue (m1-m0), K loop (m2-m1), epilogue (m4-m2)
         dur = {}
-        for a, b in ((0, 1), (1, 2), (2, 4)):
+        for a, b in ((0, 1), (1, 2), (2, 4), (2, 3), (3, 5), (5, 6), (6, 4)):
             d = [marks[i * 8 + b] - marks[i * 8 + a] for i in range(NSLOT // 8)
                  if 0 < marks[i * 8 + a] <= post and 0 < marks[i * 8 + b] <= post]
             if d:
@@ -74,7 +74,7 @@ def main():
                                           bh.variant_name(kind, dims)))
             for post, pts in one(dev, wl, args.reps)[1:]:
                 line = "  post %7.2f |" % post
-                for k in range(5):
+                for k in range(8):
                     if k in pts:
                         v = pts[k]
                         line += " m%d %6.2f/%6.2f/%6.2f (%d)" % (k, min(v), statistics.median(v), max(v), len(v))

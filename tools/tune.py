@@ -41,6 +41,8 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
+    if name.startswith("dc"):
+        return 1 << 30
     if name.startswith("gv"):
         return 16 * (int(name.split("w")[1]) if "w" in name else 4)
     return int(re.match(r"\d+", name.split("x")[2]).group(0))
@@ -103,6 +105,7 @@ def main():
                     "only if the new best is this much faster (timings vary a few %% from box to box)")
     ap.add_argument("--cfg-re", default="", help="sweep only configs matching this regex (plus the --out "
                     "table's current choice for the op, timed again, so the better one is kept)")
+    ap.add_argument("--key-re", default="", help="sweep only ops whose table key ('conv B IC H W ...') matches")
     ap.add_argument("--only-untuned", action="store_true", help="sweep only ops the --out table has no entry "
                     "for (use with --merge)")
     args = ap.parse_args()
@@ -134,7 +137,7 @@ def main():
             kind = 0 if isinstance(s, ops.SgemmShape) else 1
             dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
             key = ("sgemm " if kind == 0 else "conv ") + " ".join(map(str, dims))
-            if key in table or key in have:
+            if key in table or key in have or (args.key_re and not re.search(args.key_re, key)):
                 continue
             wl = runner.Workload(dev, [s])
             M, N, K = (s.M, s.N, s.K) if kind == 0 else (s.OC, s.B * s.OH * s.OW, s.K)
@@ -147,6 +150,10 @@ def main():
                     if args.cfg_re and not re.search(args.cfg_re, cn):
                         continue
                     nkt = -(-K // bk_of(cn))
+                    if cn.startswith("dc"):  # direct conv (stems): no K split; UNSUP for other kernels
+                        if kind == 1 and cn.startswith("dc%ds%d" % (s.KY, s.sy)) and s.KX == s.KY and s.sx == s.sy:
+                            cand.append((ci, 0))
+                        continue
                     if cn.startswith("srk"):  # stream-K: S = blocks per CU
                         cand += [(ci, 1), (ci, 2), (ci, 5), (ci, 6)]  # 5, 6: whole tiles per block
                         continue
