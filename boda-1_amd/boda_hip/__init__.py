@@ -28,7 +28,8 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
            "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
            "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
-           "bh_eltwise", "bh_conv2d_fwd_nchw_slab", "bh_conv2d_fwd_nchw_res"]
+           "bh_eltwise", "bh_conv2d_fwd_nchw_slab", "bh_conv2d_fwd_nchw_res", "bh_jit_build", "bh_jit_compile",
+           "bh_jit_launch", "bh_jit_release"]
 
 
 class BodaHipError(RuntimeError):
@@ -97,6 +98,8 @@ def lib():
         L.bh_graph_destroy.argtypes = [c_vp, ctypes.c_int]
         L.bh_tune_set.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.bh_tune_cfg_name.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+        L.bh_jit_build.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_size_t)]
         _lib = L
     return _lib
 
@@ -127,6 +130,15 @@ def conv_filts_packed_floats(s):
 
 def pool_out_size(n, k, stride, pad):
     return lib().bh_pool_out_size(n, k, stride, pad)
+
+
+def jit_build(src, opts=""):
+    """Compile a device program with hiprtc for gfx950 (no device needed); returns (code bytes, log)."""
+    log = ctypes.create_string_buffer(1 << 16)
+    n = ctypes.c_size_t(0)
+    rc = lib().bh_jit_build(src.encode(), opts.encode(), log, len(log), ctypes.byref(n))
+    _check(rc)
+    return n.value, log.value.decode(errors="replace")
 
 
 def tune_cfg_names(op_kind):

@@ -142,4 +142,5 @@ std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
 std::string conv_variant(const uint32_t *d);
 int tune_set(bh_ctx *ctx, int op, int cfg, int splits);
 int tune_cfg_name(int op, int cfg, std::string &out);
+void jit_release_all(bh_ctx *c);
 }  // namespace bh

@@ -58,12 +58,13 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   static_assert(OCT % 4 == 0 && OCT <= BREG, "16-B weight pieces, biases of one tile");
   constexpr int PF = TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3);  // LDS fragment prefetch distance (steps)
   constexpr int IS = (KK2 + 1) / 2 > 1 ? (KK2 + 1) / 2 : 1;     // steps the next stage's DMAs are spread over
-  // C staging: ER rows (a multiple of 8: one 4-register group of every MFMA tile) per pass,
-  // in the slot of the stage just consumed
-  constexpr int ER = (SLOT - BREG) / NPX >= 32 ? 32 : ((SLOT - BREG) / NPX >= 16 ? 16 : 8);
-  static_assert(ER * NPX <= SLOT - BREG, "C staging rows");
-  constexpr int CPP = ER * NPX / 4;  // float4 chunks per staging pass
-  static_assert(CPP % 256 == 0, "chunks per thread");
+  // epilogue: a lane's accumulators hold 4 consecutive pixels of one output channel per
+  // register quad (the MFMA's rows are pixels), stored as NST float4 pieces per lane, deferred
+  // into the first ISS steps of the next tile (one store per step or two): a CU retires store
+  // instructions at a limited rate, so a burst of them at the end of a tile stalls the waves
+  // while the MFMA pipe idles (cdna_hip_programming.md T21)
+  constexpr int NST = TM * TN * 4;
+  constexpr int ISS = KK2 > 2 * NST ? 2 * NST : KK2;
   // one __shared__ array only (a second object makes hipcc wait vmcnt(0) at ds_reads)
   __shared__ __attribute__((aligned(16))) float smem[D * SLOT];
 
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
     const uint32_t r = e / WPM, c = e - (e / WPM) * WPM;
     const int x = (int)c - (int)p.px;
-    srow[j] = (r < (uint32_t)RIN) & ((uint32_t)x < p.W) ? r : 0xffffu;
+    srow[j] = ((r < (uint32_t)RIN) & ((uint32_t)x < p.W)) ? r : 0xffffu;
     srel[j] = (r * p.W + (uint32_t)x) * 4u;
   }
 
@@ -138,9 +139,23 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   uint32_t poff[TN];  // this lane's pixels' strip offsets in the current tile (bytes)
   uint32_t hsel = kh ? 0xffffffffu : 0u;
 
+  // deferred stores of the previous tile: float4 piece q = (t, tn, g) of this lane, at dstore[q]
+  // (byte offset, or OOB where the piece is outside the output)
+  f32x4v dval[NST];
+  uint32_t dbase[TM], dpx = 0, dhw = 0;  // piece (t, tn, gq): byte offset dbase[t] + 4 (32 tn + 8 gq), pixel
+                                         // dpx + 32 tn + 8 gq (dropped at >= dhw: past the image)
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  auto store_one = [&](int q) {
+    const int t = q / (TN * 4), tn = (q / 4) % TN, gq = q % 4;
+    const uint32_t off = oob_unless(dpx + (uint32_t)(32 * tn + 8 * gq) < dhw, dbase[t] + (uint32_t)(32 * tn + 8 * gq) * 4u);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
+                                           rso, off, 0, 0);
+  };
+
   // one stage = one input channel of one tile: KK2 steps of TM x TN MFMAs; stage g_issue's
-  // DMAs are issued over the first IS steps; LDS fragments are read PF steps ahead
-  auto compute = [&](int slot, int islot, uint32_t g_issue) {
+  // DMAs are issued over the first IS steps, the previous tile's deferred stores (if any) over
+  // the first ISS; LDS fragments are read PF steps ahead
+  auto compute = [&](int slot, int islot, uint32_t g_issue, bool dstores) {
     uint32_t vo[LW];
     plan(g_issue, vo);
     const float *const Ab = smem + slot * SLOT + kh * KK2 * OCT + li;
@@ -164,16 +179,21 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     for (int s = 0; s < KK2; ++s) {
       if (s + PF < KK2) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+      // A = the strip (MFMA rows: pixels), B = the weights (columns: output channels)
 #pragma unroll
       for (int t = 0; t < TM; ++t)
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s % (PF + 1)][t], b[s % (PF + 1)][tn], acc[t][tn], 0, 0, 0);
+          acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)][tn], a[s % (PF + 1)][t], acc[t][tn], 0, 0, 0);
       // q in [QB(s), QB(s+1)), QB(s) = ceil(s * LW / IS): early, so that even the last DMA has
       // most of a stage to land before the wait that retires it (the very next stage at D = 2)
 #pragma unroll
       for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
         issue_one(q, islot, vo[q]);
+      if (dstores) {
+#pragma unroll
+        for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -186,16 +206,14 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #pragma unroll
     for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
   }
-  const bool vec = p.cvec != 0;
-  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const bool vec = p.cvec != 0 && !p.res;  // float4 pieces, deferred (else stored at once)
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
-  constexpr int NSTW = TM * (32 / ER) * (CPP / 256);  // float4 stores per wave per tile
-  bool after_epi = false;
+  bool pending = false;  // deferred stores of the previous tile not yet issued
   int slot = 0;
   uint32_t g = 0;
   // outer loop over the block's tiles, inner over a tile's input channels (nested: the
   // accumulators stay in AGPRs); the ring runs on across tiles, so the next tile's first stage
-  // lands while this tile's epilogue stores go out
+  // lands while this tile's epilogue runs, and its stores go out during the next tile
   for (uint32_t i = 0; i < my_tiles; ++i) {
     uint32_t oc0, img, p0;
     decode(b0 + i * G, oc0, img, p0);
@@ -214,80 +232,73 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
         for (int r = 0; r < 16; ++r) acc[t][tn][r] = 0.0f;
     int cslot = 0;
     for (uint32_t ic = 0; ic < p.IC; ++ic, ++g) {
-      // the first stage of a tile after an epilogue: that epilogue's stores (younger than this
-      // stage's DMAs) may stay in flight
-      if (after_epi && ic == 0) vm_wait<((D - 2) * LW + NSTW < 63 ? (D - 2) * LW + NSTW : 63)>();
-      else vm_wait<(D - 2) * LW>();
+      vm_wait<(D - 2) * LW>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage g landed for all waves; all done reading g-1
       asm volatile("" ::: "memory");
       if (i == 0 && ic == 0) KT(1);
       if (i == 1 && ic == 0) KT(5);
-      compute(slot, slot == 0 ? D - 1 : slot - 1, g + D - 1);  // + stage g+D-1 into slot (g-1) % D
+      // + stage g+D-1 into slot (g-1) % D, and in a tile's first stage the previous tile's stores
+      compute(slot, slot == 0 ? D - 1 : slot - 1, g + D - 1, pending);
+      pending = false;
       cslot = slot;
       slot = slot == D - 1 ? 0 : slot + 1;
     }
     if (i == 0) KT(2);
     if (i == 1) KT(6);
 
-    // ---- epilogue through LDS, in the slot of the stage just consumed (no DMA targets it
-    // before the next stage's compute): ER rows of every MFMA tile at a time are written by
-    // fragment, then read back row-major and stored as 16-B pieces -- a wave instruction
-    // writes one 1-KB output row run, a quarter of the store instructions of per-fragment
-    // dword stores (the store issue bounds such an epilogue: cdna_hip_programming.md T21)
-    float *const Cs = smem + cslot * SLOT;
+    // ---- epilogue. acc[t][tn][4*gq + e] is output channel oc0 + 32 t + li, pixel
+    // p0 + wave*32*TN + 32 tn + 8 gq + 4 kh + e (e = 0..3): bias (from the consumed slot: no DMA
+    // targets it before the next stage's compute), ReLU, then 16-B pieces -- deferred into the
+    // next tile's first stage, or stored now if this is the block's last tile. With a residual
+    // or an output whose pixel runs are not 16-B pieces: element stores now.
     const float *const Lb = smem + cslot * SLOT + WREG + SREG;
     const uint32_t obase = img * p.OCOHW;
+    if (vec) {
+      dpx = p0 + (uint32_t)(wave * 32 * TN + 4 * kh);
+      dhw = p.OHW;
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-#pragma unroll
-      for (int h = 0; h < 32 / ER; ++h) {
-        // raw barriers: a __syncthreads() would also wait (vmcnt(0)) for the next stage's DMAs
-        // and this epilogue's own stores, which may stay in flight
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave is done reading the slot (stage operands / previous pass)
-        asm volatile("" ::: "memory");
+      for (int t = 0; t < TM; ++t) {
+        const uint32_t m = oc0 + 32 * t + li;
+        const float bb = Lb[32 * t + li];
+        dbase[t] = oob_unless(m < p.M, (obase + m * p.OHW + dpx) * 4u);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-          for (int r = h * (ER / 2); r < (h + 1) * (ER / 2); ++r)
-            Cs[((r & 3) + 8 * (r >> 2) + 4 * kh - h * ER) * NPX + wave * 32 * TN + 32 * tn + li] = acc[t][tn][r];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        // buffer stores with misses for dead lanes (no branches): every wave issues exactly
-        // NSTW store instructions per tile on the float4 path, which the next tile's first
-        // stage wait leaves in flight
+          for (int gq = 0; gq < 4; ++gq) {
+            f32x4v v;
 #pragma unroll
-        for (int j = 0; j < CPP / 256; ++j) {
-          const int c = tid + 256 * j, row = c / (NPX / 4), col = 4 * (c % (NPX / 4));
-          const int trow = 32 * t + h * ER + row;
-          const uint32_t m = oc0 + (uint32_t)trow, px = p0 + (uint32_t)col;
-          const bool live = (m < p.M) & (px < p.OHW);
-          f32x4v v = *(const f32x4v *)&Cs[row * NPX + col];
-          const float bb = Lb[trow];
-          const uint32_t o = obase + m * p.OHW + px;  // (host: the output is < 2 GiB)
-          if (vec) {
-            v += bb;
-            if (p.res) v += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsr, oob_unless(live, o * 4u), 0, 0));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = (p.relu && v[q] < 0.0f) ? 0.0f : v[q];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                                   rso, oob_unless(live, o * 4u), 0, 0);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const uint32_t oq = oob_unless(live & (px + q < p.OHW), (o + q) * 4u);
-              float x = v[q] + bb;
-              if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, oq, 0, 0));
-              x = (p.relu && x < 0.0f) ? 0.0f : x;
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, oq, 0, 0);
+            for (int e = 0; e < 4; ++e) {
+              const float x = acc[t][tn][4 * gq + e] + bb;
+              v[e] = (p.relu && x < 0.0f) ? 0.0f : x;
             }
+            dval[(t * TN + tn) * 4 + gq] = v;
           }
-        }
+      }
+      if (i + 1 < my_tiles) {
+        pending = true;
+      } else {
+#pragma unroll
+        for (int q = 0; q < NST; ++q) store_one(q);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const uint32_t m = oc0 + 32 * t + li;
+        const float bb = Lb[32 * t + li];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t px = p0 + (uint32_t)(wave * 32 * TN + 32 * tn + 8 * (r >> 2) + 4 * kh + (r & 3));
+            const uint32_t o = oob_unless((m < p.M) & (px < p.OHW), (obase + m * p.OHW + px) * 4u);
+            float x = acc[t][tn][r] + bb;
+            if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
+            x = (p.relu && x < 0.0f) ? 0.0f : x;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, 0);
+          }
       }
     }
-    after_epi = true;
     if (i == 0) KT(3);
   }
   vm_wait<0>();
@@ -323,7 +334,6 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2>("dc11s4x96d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2>("dc11s4x32d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3>("dc11s4x32d3"),
-      dc_cfg<11, 11, 4, 228, 31, 1, 2, 2>("dc11s4x32n256d2"),
       // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
       dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
       dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),

@@ -240,6 +240,57 @@ __device__ __forceinline__ void combine_tile(const GemmArgs &p, uint32_t tile, u
   }
 }
 
+// LDS-staged tile epilogue. Per-fragment stores from the MFMA accumulators move 128-256 B per
+// store instruction, and a CU retires store instructions at a roughly fixed rate whatever their
+// width (cdna_hip_programming.md T21: the store ISSUE bounds such an epilogue) -- a 64 KB tile
+// took several microseconds. Here the waves' accumulators go to LDS row-major (the ring is
+// dead: the caller has drained every DMA), and every thread then takes float4 chunks c of the
+// BM x BN tile (row 4c / BN), handing each to f(c, value): one 16-B store per lane, 1 KB per
+// wave instruction. Accumulator map of the tile kernels: acc[i][j][r] is row
+// wm*WM + TM*((r&3) + 8*(r>>2) + 4*kh) + i, column wn*WN + TN*li + j.
+// If the LDS cannot hold the whole tile (BM*BN > LDSF floats), it goes in two halves of BM/2
+// rows (waves of one wave-row each). Ends with every thread past its last LDS read.
+template <int BM, int BN, int TM, int TN, int WAVES_N, int NT, int LDSF, class F>
+__device__ __forceinline__ void staged_epilogue(float *lds, f32x16 (&acc)[TM][TN], int wave, int lane, int tid,
+                                                F &&f) {
+  constexpr int WM = 32 * TM, WN = 32 * TN;
+  constexpr int WAVES_M = NT / 64 / WAVES_N;
+  constexpr int PASSES = BM * BN <= LDSF ? 1 : 2;
+  static_assert(PASSES == 1 || (WAVES_M == 2 && (BM / 2) * BN <= LDSF), "staged epilogue: LDS too small");
+  constexpr int PR = BM / PASSES;          // rows per pass
+  constexpr int CPP = PR * BN / 4;         // float4 chunks per pass
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N, kh = lane >> 5, li = lane & 31;
+#pragma unroll
+  for (int h = 0; h < PASSES; ++h) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave done with the LDS (ring reads / previous pass)
+    asm volatile("" ::: "memory");
+    if (PASSES == 1 || wm == h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (PASSES == 1 ? wm * WM : 0) + TM * ((r & 3) + 8 * (r >> 2) + 4 * kh) + i;
+          typename fvec<TN>::t w;
+          if constexpr (TN == 1) w = acc[i][0][r]; else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) w[j] = acc[i][j][r];
+          }
+          *(typename fvec<TN>::t *)&lds[row * BN + wn * WN + TN * li] = w;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < (CPP + NT - 1) / NT; ++k) {
+      const int c = tid + k * NT;
+      if (CPP % NT == 0 || c < CPP) f((uint32_t)(h * CPP + c), *(const f32x4v *)&lds[4 * c]);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

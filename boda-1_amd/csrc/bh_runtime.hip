@@ -130,6 +130,7 @@ int bh_destroy(bh_ctx *c) {
   for (hipEvent_t ev : c->events) (void)hipEventDestroy(ev);
   for (hipGraphExec_t g : c->graphs)
     if (g) (void)hipGraphExecDestroy(g);
+  bh::jit_release_all(c);
   for (void *r : c->retired) (void)hipFree(r);
   if (c->ws) (void)hipFree(c->ws);
   if (c->wpack) (void)hipFree(c->wpack);

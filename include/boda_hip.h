@@ -211,6 +211,24 @@ int bh_chan_affine(bh_ctx *ctx, const float *in, float *out, const float *scale,
                    uint32_t C, uint32_t HW, int relu);
 int bh_eltwise(bh_ctx *ctx, const float *a, const float *b, float *out, uint64_t n, int op, int relu);
 
+/* ---- generic device functions through hiprtc: what rtc_compute_t::compile / run do for every
+ *      function name the backend does not intercept (the reference JIT-compiles all CUCL with
+ *      nvrtc, src/nvrtc_util.cc:216-260, and launches it with cuLaunchKernel, :355-385). src is
+ *      the whole program (the caller prepends its CUCL prelude, as nvrtc_compute_t::compile
+ *      prepends cu_base_decls); names are the functions to look up (a missing one fails the
+ *      compile, src/nvrtc_util.cc check_runnable); opts: extra hiprtc options, space separated
+ *      (may be NULL). log (may be NULL) receives the compiler log. ----------------------------- */
+/* compile only, no device needed (code_bytes may be NULL) */
+int bh_jit_build(const char *src, const char *opts, char *log, size_t loglen, size_t *code_bytes);
+int bh_jit_compile(bh_ctx *ctx, const char *src, const char *const *names, int n, const char *opts, int *module_id,
+                   char *log, size_t loglen);
+/* 1-D launch, blks x tpb; args[i] points at the i-th kernel argument's value (a device pointer
+ * variable for a buffer, the value itself for a by-value scalar or struct) -- the reference's
+ * arg marshalling (src/nvrtc_util.cc:337-347). An event pair armed by bh_time_next_call is
+ * recorded on this launch. */
+int bh_jit_launch(bh_ctx *ctx, int module_id, const char *name, void **args, uint32_t blks, uint32_t tpb);
+int bh_jit_release(bh_ctx *ctx, int module_id);
+
 /* Name of the kernel variant bh_conv2d_fwd_nchw / bh_sgemm_kmajor would run
  * for a shape (op==0: sgemm with dims[0..2] = M,N,K; op==1: conv with
  * dims[0..10] = B,IC,H,W,OC,KY,KX,sy,sx,py,px). */
