@@ -886,7 +886,11 @@ void load_tuning() {
 choice_t heuristic(int op, const uint32_t *d, bool ring = true, bool direct = true) {
   choice_t ch;
   if (op == 0) {
-    ch.cfg = 0;
+    // big SGEMMs: the LDS-DMA ring with 128 x 128 tiles, whole K per block (tuned on
+    // sgemm-ops-full: 93-95 % of the fp32 peak from 4096^3 up); others: the tile kernel
+    const uint64_t tiles = (uint64_t)((d[0] + 127) / 128) * ((d[1] + 127) / 128);
+    ch.cfg = (ring && tiles >= 256 && d[2] >= 512) ? cfg_index(0, "r128x128x32d2") : 0;
+    ch.splits = ch.cfg > 0 ? 1 : 0;
     return ch;
   }
   uint32_t B = d[0], H = d[2], W = d[3], OC = d[4], KY = d[5], KX = d[6], sy = d[7], sx = d[8], py = d[9], px = d[10];
@@ -1113,7 +1117,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
   choice_t ch = choose(ctx, 0, d);
   if (getenv("BH_EXP_RING_DWORD_B") && vec && cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0])  // experiment
     return launch_gemm(ctx, 0, ch, A_KSCALAR, B_KSCALAR, p, "sgemm");
-  if (!vec && (!cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0] || cfgs(0)[ch.cfg].name[0] == 'r')) ch = heuristic(0, d);
+  if (!vec && (!cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0] || cfgs(0)[ch.cfg].name[0] == 'r')) ch = heuristic(0, d, false);
   return launch_gemm(ctx, 0, ch, vec ? A_KVEC : A_KSCALAR, vec ? B_KVEC : B_KSCALAR, p, "sgemm");
 }
 

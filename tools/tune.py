@@ -105,6 +105,7 @@ def main():
                     "only if the new best is this much faster (timings vary a few %% from box to box)")
     ap.add_argument("--cfg-re", default="", help="sweep only configs matching this regex (plus the --out "
                     "table's current choice for the op, timed again, so the better one is kept)")
+    ap.add_argument("--max-splits", type=int, default=64, help="largest K split count to sweep")
     ap.add_argument("--key-re", default="", help="sweep only ops whose table key ('conv B IC H W ...') matches")
     ap.add_argument("--only-untuned", action="store_true", help="sweep only ops the --out table has no entry "
                     "for (use with --merge)")
@@ -163,7 +164,7 @@ def main():
                             cand += [(ci, S) for S in [0] + SPLITS if S == 0 or nkt >= S]
                         continue
                     for S in SPLITS:
-                        if S > 1 and nkt < 2 * S:
+                        if (S > 1 and nkt < 2 * S) or S > args.max_splits:
                             continue
                         cand.append((ci, S))
                         if S > 1:
