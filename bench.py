@@ -16,6 +16,9 @@ device with the reference's gen_data mode 5 before the timed region).
   roofline    = the dominant kernel (most time): algorithmic flops per launch / its
                 average launch duration, measured with HIP events on the kernel's
                 stream around a replayed graph of back-to-back calls, vs fp32 peak
+  vendor      = per_set.*.vendor_ms: rocBLAS sgemm / MIOpen conv+bias+ReLU on the same units and
+                in the same amortized convention (libboda_hip_vendor.so), a same-node yardstick
+                only (--vendor off skips it)
   cpu_baseline= the oracle's fp32 OpenMP CPU implementation (kind "port") on a
                 bounded sample, rank 0 at N=1 only
 
@@ -121,6 +124,9 @@ def main():
     ap.add_argument("--op-timing", choices=["graph", "events"], default="graph",
                     help="per-op time: amortized over a replayed graph of back-to-back calls (default), or HIP "
                          "events bound to each call's own dispatches")
+    ap.add_argument("--vendor", choices=["on", "off"], default="on",
+                    help="also time rocBLAS sgemm / MIOpen conv(+bias+ReLU) per unit (libboda_hip_vendor.so): "
+                         "per_set.*.vendor_ms, context only")
     args = ap.parse_args()
 
     dd = Dist()
@@ -183,6 +189,19 @@ def main():
             ktime[i] = wl.op_graph_time(i, reps)
             dev.events_reset()
 
+    # Same-node comparator (context, never the target): the vendor libraries on the same units, in
+    # the same amortized back-to-back convention (src/culibs-wrap.cc:94-242 is the reference's seam).
+    vtime = [None] * nop
+    vinfo = [None] * nop
+    if args.vendor == "on":
+        from boda_hip import vendor
+        vd = vendor.Vendor(dd.local_rank % max(1, ndev))
+        for i in range(nop):
+            reps = max(3, min(50, int(round(2e-3 / max(ktime[i], 1e-6)))))
+            vinfo[i] = vd.time(my_shapes[i], reps)
+            vtime[i] = vinfo[i]["ms"] / 1e3
+        vd.close()
+
     my_flops = sum(s.flops() for s in my_shapes)
     total_flops = dd.sum(my_flops) * args.steps
     value = total_flops / elapsed / 1e9
@@ -195,7 +214,8 @@ def main():
         dims = [s.M, s.N, s.K] if kind == 0 else s.as_dims()
         recs.append({"tag": my_tags[i], "op": mine[i][0], "dims": dims, "variant": boda_hip.variant_name(kind, dims),
                      "flops": s.flops(), "bytes": s.bytes(), "kernel_s": ktime[i], "event_s": ev_time[i],
-                     "roof_s": runner.roofline_secs(s), "bound": runner.bound_of(s), "rank": dd.rank})
+                     "roof_s": runner.roofline_secs(s), "bound": runner.bound_of(s), "rank": dd.rank,
+                     "vendor_s": vtime[i], "vendor": vinfo[i]})
     recs = [r for part in dd.gather_obj(recs) for r in part]
 
     per_set = {}
@@ -206,9 +226,17 @@ def main():
         f = sum(r["flops"] for r in rs)
         t = sum(r["kernel_s"] for r in rs)
         rt = sum(r["roof_s"] for r in rs)
+        te = sum(r["event_s"] for r in rs)
         per_set[n] = {"ops": len({r["op"] for r in rs}), "gflop": round(f / 1e9, 3), "sum_kernel_ms": round(t * 1e3, 4),
                       "gflops": round(f / t / 1e9, 2), "roofline_frac": round(rt / t, 4),
-                      "roofline_ms": round(rt * 1e3, 4)}
+                      "roofline_ms": round(rt * 1e3, 4),
+                      # the reference's own per-call convention (event pair around each call)
+                      "sum_event_ms": round(te * 1e3, 4), "roofline_frac_events": round(rt / te, 4)}
+        if all(r["vendor_s"] is not None for r in rs):
+            tv = sum(r["vendor_s"] for r in rs)
+            per_set[n].update({"vendor_ms": round(tv * 1e3, 4), "vendor_roofline_frac": round(rt / tv, 4),
+                               "vendor_over_ours": round(tv / t, 3),
+                               "ops_faster_than_vendor": sum(r["kernel_s"] <= r["vendor_s"] for r in rs)})
 
     # dominant kernel: the variant with the most time over the whole job
     by_var = {}
@@ -242,6 +270,7 @@ def main():
     if args.per_op and dd.rank == 0:
         with open(args.per_op, "w") as f:
             json.dump([dict(r, kernel_ms=r["kernel_s"] * 1e3, event_ms=r["event_s"] * 1e3,
+                            vendor_ms=None if r["vendor_s"] is None else r["vendor_s"] * 1e3,
                             gflops=r["flops"] / r["kernel_s"] / 1e9, roofline_frac=r["roof_s"] / r["kernel_s"])
                        for r in recs], f, indent=0)
 
@@ -266,7 +295,10 @@ def main():
                        "lpt_imbalance_predicted": round(pred_imb, 4),
                        "lpt_imbalance_measured": round(imbalance(rank_times), 4),
                        "shared_device": shared,
-                       "plat": dev.plat_tag()},
+                       "plat": dev.plat_tag(),
+                       "vendor": ("rocblas_sgemm / MIOpen Find-chosen conv fwd + miopenOpTensor bias + "
+                                  "miopenActivationForward ReLU, same units, amortized back-to-back calls, "
+                                  "context only" if args.vendor == "on" else None)},
             "per_set": per_set,
             "roofline": roof,
             "cpu_baseline": cpu,

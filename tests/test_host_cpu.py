@@ -112,3 +112,18 @@ def test_inconsistent_ops_rejected():
            "y=55,x=55),in_pad=(y=0,x=0),kern_sz=(y=1,x=1),out=(img=3,chan=16,y=54,x=55),stride=(y=1,x=1)))")
     with pytest.raises(ValueError):
         ops.conv_shape(ops.parse_op(bad))
+
+
+def test_vendor_library_exports_every_symbol():
+    """The comparator library (include/boda_hip_vendor.h) loads and exports its C-ABI; the product
+    library does not link rocBLAS/MIOpen."""
+    from boda_hip import vendor
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "boda_hip_vendor.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(bhv_[a-z0-9_]+)\s*\(", txt)))
+    assert syms == sorted(vendor.EXPORTS)
+    lib = ctypes.CDLL(vendor.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+    deps = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-d", boda_hip.LIB_PATH], capture_output=True,
+                          text=True).stdout
+    assert "rocblas" not in deps.lower() and "miopen" not in deps.lower()

@@ -7,7 +7,7 @@ set -eu
 out=$1; dest=$2
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$out/bench.json"
+timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --vendor off > "$out/bench.json"
 python3 tools/traffic_shapes.py "$out/bench.json" > "$out/shapes.txt"
 i=0
 while read -r kind dims; do
