@@ -1,0 +1,467 @@
+// bh_dcm.hip -- direct convolution for stride-1 convs with many input channels (3x3 p1, 5x5 p2:
+// most of the conv set's MFMA-bound time).
+//
+// As an implicit GEMM (the ring kernels) every K row of every stage is a separate 64-column
+// dword LDS-DMA gather of one input row segment: a 128-pixel x 32-deep B tile takes 64 DMA
+// instructions, 0.31 DMA issues per MFMA, and those issues (not the data) hold the MFMA pipe
+// at ~75 % of peak (PMC, profiles/r02). Here a stage is CI INPUT CHANNELS of one tile:
+//  * the channels' weights [CI][KY*KX][OCT] (16-B LDS-DMA from the packed k-major bank of
+//    bh_conv_filts_pack) and their input strip [CI][RIN][WPM] -- the input rows the tile's
+//    pixels touch, WPM = W rounded up to 4, rows above / below the image zero (OOB misses),
+//    filled by 16-B LDS-DMA of row pieces: every input element of the strip is fetched once
+//    per tile, not once per filter tap (KY*KX times), at ~0.08 DMA issues per MFMA (an LDS-DMA
+//    issue costs the wave ~60-180 cycles: cdna_hip_programming.md, the ring kernels' limit).
+//    Columns left / right of the image are not materialised: a tap that falls there reads a
+//    neighbouring element and is zeroed by a per-lane select (the pixel's column is fixed);
+//  * a tile is OCT = 32*TM output channels x NPX = 128*TN consecutive output pixels of the
+//    flattened (image, oy, ox) space -- tiles run across image boundaries, so small images
+//    (13x13, 7x7) waste no MFMA rows. The strip's rows are "virtual" padded input rows
+//    img*(H+2py) + iy + py: one pixel's taps are one linear offset ky*WPM + kx from its base;
+//  * v_mfma_f32_32x32x2_f32 (exact fp32) with A = the strip (MFMA rows: pixels), B = the
+//    weights (columns: output channels); lane half h takes channels h*CI/2 .. of the stage, so
+//    both halves read at the same compile-time offsets from a per-lane base: a fragment is one
+//    ds_read_b32 with an immediate offset, no index arithmetic;
+//  * a persistent grid shares the op's (tile, stage) iterations equally between blocks
+//    (stream-K, as srk_kernel in bh_ring.hip): tiles cut between blocks are summed by their last
+//    arriving block in block order (bitwise reproducible); the DMA ring runs on across tiles.
+// Same GemmArgs contract as the other conv kernels (a = packed bank, lda = OC4; b = input;
+// OCOHW = the output's image stride, so channel-slab outputs work).
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+namespace {
+
+// logical block of hardware block bid: blocks b, b+8, ... share an XCD under round-robin
+// placement, so give each XCD a contiguous run of iterations (its L2 sees neighbouring tiles)
+__device__ __forceinline__ uint32_t dcm_lb(uint32_t bid, uint32_t G) {
+  const uint32_t xcd = bid & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int KY, int KX, int SL, int CI, int TM, int TN, int D>
+__global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
+  constexpr int NW = 4, NT = 256;
+  constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
+  constexpr int KK = KY * KX, CH2 = CI / 2, STEPS = CH2 * KK;
+  constexpr int WPC = CI * KK * OCT / 4;                 // 16-B weight pieces per stage
+  constexpr int LWA = (WPC + NW * 64 - 1) / (NW * 64);   // weight DMA instructions per wave
+  constexpr int WREG = LWA * NW * 256;                   // floats
+  // one channel's strip: RIN x WPM floats at run time (p.ldc = RIN * WPM <= SL, p.ldb = WPM,
+  // WPM % 4 == 0), loaded in 16-B pieces
+  static_assert(SL % 4 == 0, "16-B strip pieces");
+  constexpr int LWB = (CI * SL / 4 + NW * 64 - 1) / (NW * 64);
+  constexpr int SREG = LWB * NW * 256;
+  constexpr int BREG = NW * 64;                          // the tile's biases, one DMA per wave
+  constexpr int SLOT = WREG + SREG + BREG;
+  constexpr int LW = LWA + LWB + 1;
+  static_assert(CI % 2 == 0, "channel halves");
+  static_assert(D >= 2 && (D - 2) * LW <= 63, "vmcnt range");
+  static_assert(OCT % 4 == 0 && OCT <= BREG, "16-B weight pieces, biases of one tile");
+  constexpr int PF = TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3);  // LDS fragment prefetch (steps)
+  constexpr int IS = STEPS > 3 ? STEPS / 2 : 1;                   // steps the next stage's DMAs spread over
+  constexpr int NQ = TM * TN * 4;                                 // float4 pieces of a lane's accumulators
+
+  // one __shared__ array only (a second object makes hipcc wait vmcnt(0) at ds_reads)
+  __shared__ __attribute__((aligned(16))) float smem[D * SLOT + 4];
+  uint32_t *const flag = (uint32_t *)(smem + D * SLOT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = lane >> 5, li = lane & 31;
+  KT(0);
+
+  const uint32_t lb = dcm_lb(blockIdx.x, gridDim.x);
+  const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
+  const uint32_t Hp = p.H + 2 * p.py;
+  const uint32_t WPM = p.ldb, SLICE = p.ldc;
+
+  // tile t: OC tile fastest (consecutive tiles share the input strip through L2)
+  auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &n0) {
+    const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);  // tiles_m = OC tiles
+    oc0 = (t - pt * p.tiles_m) * OCT;
+    n0 = pt * NPX;
+  };
+  // virtual padded input row of the first strip row of the tile starting at pixel n0
+  auto vrow0 = [&](uint32_t n0) -> uint32_t {
+    const uint32_t img = fdiv(n0, p.ohw_m, p.ohw_s), pix = n0 - img * p.OHW;
+    return img * Hp + fdiv(pix, p.ow_m, p.ow_s);
+  };
+
+  // ---- tile-independent per-lane parts of the DMA source offsets
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+  // weight piece e of the [CI][KK][OCT] image: packed-bank row tap*IC + (ic0 + c), column 4*c4
+  uint32_t wrel[LWA], wc4[LWA];  // wc4 = 0xffff: a piece past the image (never loads)
+#pragma unroll
+  for (int j = 0; j < LWA; ++j) {
+    const uint32_t e = (uint32_t)((wave * LWA + j) * 64 + lane);
+    const uint32_t row = e / (OCT / 4), c4 = e % (OCT / 4);
+    const uint32_t c = row / KK, tap = row % KK;
+    wc4[j] = row < (uint32_t)(CI * KK) ? 4 * c4 : 0xffffu;
+    wrel[j] = ((tap * p.IC + c) * p.lda + 4 * c4) * 4u;
+  }
+  // strip piece e of the [CI][RIN][WPM] image: channel c, strip row r, input columns 4*x4 ..
+  // 4*x4 + 3 (a piece's tail past the row end reads the next row: only masked taps read it)
+  uint32_t sr[LWB], sx[LWB];  // sx = channel offset + input column, or 0xffffffff (never loads)
+#pragma unroll
+  for (int j = 0; j < LWB; ++j) {
+    const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
+    const uint32_t c = e / (SLICE / 4), rem = e - c * (SLICE / 4);
+    const uint32_t r = rem / (WPM / 4), x4 = rem - r * (WPM / 4);
+    sr[j] = r;
+    sx[j] = c < (uint32_t)CI ? c * p.HW + 4 * x4 : 0xffffffffu;
+  }
+  // the strip offsets of the tile being issued (channel 0 of the stage; OOB where the element
+  // is padding or past the images), recomputed only when the issue side enters a new tile
+  uint32_t srel[LWB];
+  uint32_t ls_tile = 0xffffffffu;
+
+  // Source offsets of this wave's LW DMA instructions for iteration `it` (tile it / ipt, channel
+  // group it % ipt); iterations past the block's range are all misses (OOB zeros, no memory
+  // traffic) so every wave always has the same number in flight and nothing branches
+  auto plan = [&](uint32_t it, uint32_t (&vo)[LW]) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * CI;
+    uint32_t oc0, n0;
+    tile_of(t, oc0, n0);
+    const uint32_t dead = it < it1 ? 0u : OOB;
+    const uint32_t wlim = p.lda - min(oc0, p.lda), wb = (oc0 + ic0 * p.lda) * 4u;
+#pragma unroll
+    for (int j = 0; j < LWA; ++j) vo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
+    if (t != ls_tile) {  // uniform
+      const uint32_t v0 = vrow0(n0);
+#pragma unroll
+      for (int j = 0; j < LWB; ++j) {
+        const uint32_t vr = v0 + sr[j];
+        const uint32_t img = fdiv(vr, p.kyx_m, p.kyx_s);  // kyx fastdiv = H + 2py here
+        const uint32_t iy = vr - img * Hp - p.py;         // wraps (misses) in the top padding
+        const bool ok = (sx[j] != 0xffffffffu) & (iy < p.H) & (img < p.tiles_n);  // tiles_n = images
+        srel[j] = oob_unless(ok, (img * p.ICHW + iy * p.W + sx[j]) * 4u);
+      }
+      ls_tile = t;
+    }
+    // + the stage's channel offset: an OOB offset stays >= 2^31 (a miss)
+    const uint32_t chw4 = ic0 * p.HW * 4u;
+#pragma unroll
+    for (int j = 0; j < LWB; ++j) vo[LWA + j] = (srel[j] + chw4) | dead;
+    const uint32_t bo = (uint32_t)(64 * wave + lane);
+    vo[LW - 1] = oob_unless((bo < (uint32_t)OCT) & (oc0 + bo < p.M), (oc0 + bo) * 4u) | dead;
+  };
+  auto issue_one = [&](int q, int slot, uint32_t vo) {
+    float *const base = smem + slot * SLOT;
+    if (q < LWA) dma16(rsw, base + (wave * LWA + q) * 256, vo);
+    else if (q < LWA + LWB) dma16(rsi, base + WREG + (wave * LWB + q - LWA) * 256, vo);
+    else dma4(rsbias, base + WREG + SREG + 64 * wave, vo);
+  };
+
+  f32x16 acc[TM][TN];
+  uint32_t poff[TN];  // this lane's pixels' strip offsets in the current tile (bytes), half included
+  uint32_t xin[TN];   // bit kx: the pixel's tap column kx is inside the image
+
+  // one stage = CI channels of one tile: STEPS steps of TM x TN MFMAs; iteration it_issue's DMAs
+  // go out over the first IS steps; LDS fragments are read PF steps ahead
+  auto compute = [&](int slot, int islot, uint32_t it_issue) {
+    uint32_t vo[LW];
+    plan(it_issue, vo);
+    const float *const Ab = smem + slot * SLOT + kh * (CH2 * KK * OCT) + li;
+    const char *const Sb = (const char *)(smem + slot * SLOT + WREG);
+    auto frag = [&](int s, float (&a)[TM], float (&b)[TN]) {
+      const int cc = s / KK, tap = s % KK;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a[t] = Ab[(cc * KK + tap) * OCT + 32 * t];
+      // row base (run-time pitch) + the tap's column as an immediate offset
+      const uint32_t ro = (uint32_t)cc * SLICE * 4u + (uint32_t)(tap / KX) * WPM * 4u;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(Sb + (poff[tn] + ro) + (tap % KX) * 4);
+    };
+    float a[PF + 1][TM], b[PF + 1][TN];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) frag(s, a[s], b[s]);
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      if (s + PF < STEPS) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+      // taps left / right of the image read a neighbouring element: zero them here, at the
+      // use (a select next to the load would make the prefetch wait for the LDS latency)
+      float bm[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) bm[tn] = (xin[tn] >> ((s % KK) % KX)) & 1u ? b[s % (PF + 1)][tn] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(bm[tn], a[s % (PF + 1)][t], acc[t][tn], 0, 0, 0);
+#pragma unroll
+      for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
+        issue_one(q, islot, vo[q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  const bool vec = p.cvec != 0 && !p.res;  // float4 pixel quads (OHW % 4 == 0: a quad is in one image)
+
+  // bias, residual, ReLU and store of a tile's values: v[q], q = (t, tn, gq) holds output channel
+  // oc0 + 32 t + li, pixels n0 + wave*32*TN + 32 tn + 8 gq + 4 kh + e (e = 0..3)
+  auto store_tile = [&](uint32_t oc0, uint32_t n0, const float *Lb, f32x4v (&v)[NQ]) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const uint32_t m = oc0 + 32 * t + li;
+      const float bb = Lb[32 * t + li];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          f32x4v x = v[(t * TN + tn) * 4 + gq];
+          const uint32_t nq = n0 + (uint32_t)(wave * 32 * TN + 32 * tn + 8 * gq + 4 * kh);
+          if (vec) {
+            const uint32_t img = fdiv(nq, p.ohw_m, p.ohw_s);
+            const uint32_t o = oob_unless((m < p.M) & (nq < p.N), (img * p.OCOHW + m * p.OHW + nq - img * p.OHW) * 4u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              x[e] += bb;
+              x[e] = (p.relu && x[e] < 0.0f) ? 0.0f : x[e];
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, x),
+                                                   rso, o, 0, 0);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t n = nq + e;
+              const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+              const uint32_t o = oob_unless((m < p.M) & (n < p.N), (img * p.OCOHW + m * p.OHW + n - img * p.OHW) * 4u);
+              float y = x[e] + bb;
+              if (p.res) y += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
+              y = (p.relu && y < 0.0f) ? 0.0f : y;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, y), rso, o, 0, 0);
+            }
+          }
+        }
+    }
+  };
+
+  // tile t is done in this block (iterations [max(it0, t*ipt), min(it1, (t+1)*ipt)) are in acc):
+  // store it, or hand the partial tile over through this block's slab and the tile's ticket
+  auto finish_tile = [&](uint32_t t, int cslot) {
+    uint32_t oc0, n0;
+    tile_of(t, oc0, n0);
+    const float *const Lb = smem + cslot * SLOT + WREG + SREG;
+    f32x4v v[NQ];
+#pragma unroll
+    for (int t2 = 0; t2 < TM; ++t2)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[(t2 * TN + tn) * 4 + gq][e] = acc[t2][tn][4 * gq + e];
+    const uint32_t tb = t * p.ipt;
+    if (tb >= it0 && tb + p.ipt <= it1) {
+      store_tile(oc0, n0, Lb, v);
+      return;
+    }
+    // partial tile: slab (block, slot 0 = the block's first tile, 1 = its last), write-through
+    const uint32_t sl = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (NQ * NT * 4), NQ * NT * 16);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[q]), rw,
+                                             (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
+    const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == b1 - b0 ? 1u : 0u;
+      if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+    const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t b = b0; b <= b1; ++b) {  // block order = k order: bitwise reproducible
+      const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+      const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
+      f32x4v x[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        x[q] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rall, base + (uint32_t)((q * NT + tid) * 16),
+                                                                                 0, AUX_SC1));
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[q] += x[q];
+    }
+    store_tile(oc0, n0, Lb, v);
+  };
+
+  // ---- prologue: iterations it0 .. it0+D-2 in flight
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) {
+    uint32_t vo[LW];
+    plan(it0 + (uint32_t)s, vo);
+#pragma unroll
+    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+  }
+  int slot = 0;
+  uint32_t it = it0;
+  // outer loop over the block's tiles, inner over the tile's channel groups in this block's
+  // range (nested: the accumulators stay in AGPRs); the ring runs on across tiles
+  while (it < it1) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    const uint32_t iend = min(it1, (t + 1) * p.ipt);
+    uint32_t oc0, n0;
+    tile_of(t, oc0, n0);
+    const uint32_t v0 = vrow0(n0);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const uint32_t n = n0 + (uint32_t)(wave * 32 * TN + 32 * tn + li);
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+      const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
+      // pixels past the op read strip position 0 (their results are dropped)
+      // (ox - px may be negative: the strip follows the weight region, so such an address is
+      // still inside the slot; the tap is masked)
+      poff[tn] = n < p.N ? ((img * Hp + oy - v0) * WPM + ox - p.px) * 4u : 0u;
+      poff[tn] += (uint32_t)kh * CH2 * SLICE * 4u;
+      uint32_t m = 0;
+#pragma unroll
+      for (int kx = 0; kx < KX; ++kx) m |= ((ox + (uint32_t)kx - p.px) < p.W ? 1u : 0u) << kx;
+      xin[tn] = m;
+    }
+#pragma unroll
+    for (int t2 = 0; t2 < TM; ++t2)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t2][tn][r] = 0.0f;
+    int cslot = 0;
+    for (; it < iend; ++it) {
+      vm_wait<(D - 2) * LW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage it landed for all waves; all done reading it-1
+      asm volatile("" ::: "memory");
+      if (it == it0) KT(1);
+      compute(slot, slot == 0 ? D - 1 : slot - 1, it + D - 1);  // + stage it+D-1 into slot (it-1) % D
+      cslot = slot;
+      slot = slot == D - 1 ? 0 : slot + 1;
+    }
+    if (t == fdiv(it0, p.ipt_m, p.ipt_s)) KT(2);
+    finish_tile(t, cslot);
+  }
+  vm_wait<0>();
+#ifdef BH_KTRACE
+  KT(4);
+#endif
+}
+
+template <int KY, int KX, int SL, int CI, int TM, int TN, int D>
+cfg_t dcm_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 128 * TN, CI * KY * KX, 256, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = dcm_kernel<KY, KX, SL, CI, TM, TN, D>;
+  c.dc = 2;
+  c.dc_ky = KY;
+  c.dc_kx = KX;
+  c.dc_s = 1;
+  c.dc_wpm = SL;  // strip floats per channel (rows x run-time pitch)
+  c.dc_rin = 0;
+  c.dc_ci = CI;
+  return c;
+}
+
+}  // namespace
+
+std::vector<cfg_t> dcm_cfgs() {
+  return {
+      // 3x3. Strip capacity per channel (rows x pitch): 256 floats: 13x13 / 14x14 (16 x <= 15
+      // rows), 28x28 (28 x 9); 448: 56x56 (56 x 8), 6x6 / 7x7 (8 x <= 41 rows over 4-5 images).
+      // Most fit two blocks per CU (<= 80 KB): two waves per SIMD hide each other's barrier,
+      // LDS-latency and DMA-issue stalls, which one wave per SIMD leaves as MFMA idle time.
+      dcm_cfg<3, 3, 256, 8, 4, 1, 3>("dm3s256x128c8"),
+      dcm_cfg<3, 3, 256, 8, 2, 1, 2>("dm3s256x64c8"),
+      dcm_cfg<3, 3, 256, 8, 3, 1, 2>("dm3s256x96c8"),
+      dcm_cfg<3, 3, 256, 4, 4, 1, 3>("dm3s256x128c4"),
+      dcm_cfg<3, 3, 448, 8, 2, 1, 2>("dm3s448x64c8"),
+      dcm_cfg<3, 3, 448, 4, 4, 1, 2>("dm3s448x128c4"),
+      dcm_cfg<3, 3, 448, 4, 3, 1, 3>("dm3s448x96c4"),
+      // 5x5: 27x27 / 28x28 (28 x <= 14 rows), 14x14 (16 x <= 19)
+      dcm_cfg<5, 5, 400, 4, 4, 1, 2>("dm5s400x128c4"),
+      dcm_cfg<5, 5, 400, 4, 2, 1, 2>("dm5s400x64c4"),
+      dcm_cfg<5, 5, 400, 2, 4, 1, 3>("dm5s400x128c2"),
+  };
+}
+
+// Launch a multi-channel direct-conv configuration (p filled by launch_conv with a = packed
+// bank): UNSUP unless the shape is this instantiation's kernel at stride 1 with IC a multiple
+// of its channel group and every tile's strip fitting. splits: 0 / 1..4 = blocks per CU with
+// the (tile, channel group) iterations dealt equally; 5..8 = blocks per CU 1..4, whole tiles
+// per block.
+int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+               uint32_t sx, uint32_t splits, bool first) {
+  if ((int)KY != c.dc_ky || (int)KX != c.dc_kx || sy != 1 || sx != 1)
+    return bh::fail(BH_UNSUP, std::string("conv: direct config ") + c.name + " is for another kernel / stride");
+  if (p.IC % (uint32_t)c.dc_ci)
+    return bh::fail(BH_UNSUP, std::string("conv: input channels not a multiple of ") + c.name + "'s group");
+  const uint32_t npx = (uint32_t)c.BN, OW = p.OW, OHW = p.OHW, Hp = p.H + 2 * p.py;
+  // strip pitch: the input row rounded up to 16-B pieces (no horizontal padding: masked taps)
+  if (p.px >= (uint32_t)c.dc_kx) return bh::fail(BH_UNSUP, "conv: horizontal padding of a whole kernel");
+  const uint32_t wpm = (p.W + 3) & ~3u;
+  const uint32_t ptiles = (p.N + npx - 1) / npx;
+  // strip rows the worst pixel tile touches (virtual padded rows img*Hp + oy .. + KY - 1)
+  uint32_t rin = 0;
+  for (uint32_t t = 0; t < ptiles; ++t) {
+    const uint32_t a = t * npx, b = std::min(p.N, a + npx) - 1;
+    const uint32_t va = (a / OHW) * Hp + (a % OHW) / OW, vb = (b / OHW) * Hp + (b % OHW) / OW;
+    rin = std::max(rin, vb - va + KY);
+  }
+  if ((uint64_t)rin * wpm > (uint64_t)c.dc_wpm)
+    return bh::fail(BH_UNSUP, std::string("conv: pixel tile's input strip too large for ") + c.name);
+  p.ldb = wpm;
+  p.ldc = rin * wpm;
+  const uint64_t out_bytes = (uint64_t)B * p.OCOHW * 4;
+  if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the direct kernel");
+  p.c_bytes = (uint32_t)out_bytes;
+  const uint32_t octiles = (p.M + c.BM - 1) / c.BM;
+  const uint32_t ipt = p.IC / (uint32_t)c.dc_ci;
+  const uint64_t ntile = (uint64_t)ptiles * octiles, total = ntile * ipt;
+  if (total >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many iterations");
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256, 0) != hipSuccess || occ < 1) occ = 1;
+  const bool whole = splits > 4;
+  uint32_t bpc = splits ? (whole ? splits - 4 : splits) : 2;
+  bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  uint64_t G = (uint64_t)ncu * bpc;
+  uint32_t ipb = (uint32_t)((total + G - 1) / G);
+  if (whole) ipb = (uint32_t)((ntile + G - 1) / G) * ipt;
+  G = (total + ipb - 1) / ipb;
+  p.ipt = ipt;
+  p.ipb = ipb;
+  p.total_it = (uint32_t)total;
+  p.tiles_m = octiles;
+  p.tiles_n = B;  // images (strip rows past the last image miss)
+  bh::fastdiv f = bh::make_fastdiv(ipt);
+  p.ipt_m = f.m;
+  p.ipt_s = f.s;
+  f = bh::make_fastdiv(octiles);
+  p.tm_m = f.m;
+  p.tm_s = f.s;
+  f = bh::make_fastdiv(Hp);
+  p.kyx_m = f.m;
+  p.kyx_s = f.s;
+  const uint32_t NQ4 = (uint32_t)(c.BM / 32) * (uint32_t)(c.BN / 128) * 4;  // float4 pieces per lane
+  int rc = ensure_ws(ctx, (size_t)2 * G * NQ4 * 256 * 16);
+  if (rc == BH_OK) rc = ensure_cnt(ctx, (size_t)ntile);
+  if (rc != BH_OK) return rc;
+  p.ws = (float *)ctx->ws;
+  p.cnt = (uint32_t *)ctx->cnt;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(256), args, first, true, "conv_direct_mc");
+}
+
+}  // namespace bhk

@@ -757,6 +757,7 @@ std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
   if (op == 1) {
     for (auto const &c : gv_cfgs()) v.push_back(c);
     for (auto const &c : dc_cfgs()) v.push_back(c);
+    for (auto const &c : dcm_cfgs()) v.push_back(c);
   }
   return v;
 }
@@ -809,6 +810,9 @@ void set_fd(uint32_t d, uint32_t &m, uint32_t &s) {
   s = f.s;
 }
 
+}  // namespace
+
+namespace bhk {
 int ensure_ws(bh_ctx *ctx, size_t bytes) {
   return bh::grow_buffer(ctx, ctx->ws, ctx->ws_bytes, bytes, false, "split-K workspace");
 }
@@ -820,6 +824,9 @@ int ensure_cnt(bh_ctx *ctx, uint64_t n) {
   ctx->cnt_n = have / 4;
   return rc;
 }
+}  // namespace bhk
+
+namespace {
 
 // Number of K splits: enough blocks to cover the CUs twice, at least MIN_KT K tiles per split.
 uint32_t plan_splits(uint32_t tiles, uint32_t K, int BK, uint32_t ncu) {
@@ -1061,6 +1068,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
     s = std::string("mfma32_conv_") + (k1 ? "1x1_" : "im2col_") + c.name + ((K % 4 == 0) ? "_avec" : "_ascalar");
   }
   if (c.streamk) return s + "_streamk";
+  if (c.dc == 2) return std::string("mfma32_conv_dm_") + c.name;
   if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
   uint32_t S = resolve_splits(c, ch, M, N, K, 256);
@@ -1188,7 +1196,9 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       p.IC = IC;
       set_fd(IC, p.ic_m, p.ic_s);
       if (cfgs(1)[ch.cfg].dc) {
-        const int rc = launch_dc(ctx, cfgs(1)[ch.cfg], p, B, KY, KX, sy, sx, packed != nullptr);
+        const cfg_t &dcc = cfgs(1)[ch.cfg];
+        const int rc = dcc.dc == 2 ? launch_dcm(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, packed != nullptr)
+                                   : launch_dc(ctx, dcc, p, B, KY, KX, sy, sx, packed != nullptr);
         if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
         return launch_conv(ctx, in, filts, packed ? packed : wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py,
                            px, relu, out_ctot, res, true);

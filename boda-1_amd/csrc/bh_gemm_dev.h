@@ -319,6 +319,7 @@ struct cfg_t {
   int gv = 0;         // filter-streaming kernel (bh_gv.hip): grid (M / BM) x K chunks, BN >= N
   int dc = 0;         // direct conv (bh_direct.hip): kernel dc_ky x dc_kx, stride dc_s, strip dc_rin x dc_wpm
   int dc_ky = 0, dc_kx = 0, dc_s = 0, dc_wpm = 0, dc_rin = 0;
+  int dc_ci = 0;      // dc == 2 (bh_dcm.hip): input channels per stage
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and
@@ -330,6 +331,13 @@ std::vector<cfg_t> gv_cfgs();
 std::vector<cfg_t> dc_cfgs();
 int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
               uint32_t sx, bool first);
+// bh_dcm.hip: multi-channel direct-conv configurations for stride-1 3x3 / 5x5 convs
+std::vector<cfg_t> dcm_cfgs();
+int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+               uint32_t sx, uint32_t splits, bool first);
+// split-K / stream-K workspace and arrival tickets of the context (bh_gemm.hip)
+int ensure_ws(bh_ctx *ctx, size_t bytes);
+int ensure_cnt(bh_ctx *ctx, uint64_t n);
 int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint32_t IC, uint32_t KYX, bool first,
                        bool last);
 int ensure_wpack(bh_ctx *ctx, size_t bytes);

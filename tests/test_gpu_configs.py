@@ -33,7 +33,7 @@ CONV_SHAPES = [
 
 
 # direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py
-@pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1)) if not n.startswith("dc")],
+@pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1)) if not n.startswith(("dc", "dm"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):

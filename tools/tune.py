@@ -41,7 +41,7 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
-    if name.startswith("dc"):
+    if name.startswith(("dc", "dm")):
         return 1 << 30
     if name.startswith("gv"):
         return 16 * (int(name.split("w")[1]) if "w" in name else 4)
@@ -151,6 +151,10 @@ def main():
                     if args.cfg_re and not re.search(args.cfg_re, cn):
                         continue
                     nkt = -(-K // bk_of(cn))
+                    if cn.startswith("dm"):  # multi-channel direct conv: S = grid mode as stream-K
+                        if kind == 1 and cn.startswith("dm%d" % s.KY) and s.KX == s.KY and s.sy == s.sx == 1:
+                            cand += [(ci, 1), (ci, 2), (ci, 3), (ci, 5), (ci, 6)]
+                        continue
                     if cn.startswith("dc"):  # direct conv (stems): no K split; UNSUP for other kernels
                         if kind == 1 and cn.startswith("dc%ds%d" % (s.KY, s.sy)) and s.KX == s.KY and s.sx == s.sy:
                             cand.append((ci, 0))
