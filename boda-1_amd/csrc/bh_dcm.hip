@@ -7,12 +7,13 @@
 // at ~75 % of peak (PMC, profiles/r02). Here a stage is CI INPUT CHANNELS of one tile:
 //  * the channels' weights [CI][KY*KX][OCT] (16-B LDS-DMA from the packed k-major bank of
 //    bh_conv_filts_pack) and their input strip [CI][RIN][WPM] -- the input rows the tile's
-//    pixels touch, WPM = W rounded up to 4, rows above / below the image zero (OOB misses),
-//    filled by 16-B LDS-DMA of row pieces: every input element of the strip is fetched once
-//    per tile, not once per filter tap (KY*KX times), at ~0.08 DMA issues per MFMA (an LDS-DMA
-//    issue costs the wave ~60-180 cycles: cdna_hip_programming.md, the ring kernels' limit).
-//    Columns left / right of the image are not materialised: a tap that falls there reads a
-//    neighbouring element and is zeroed by a per-lane select (the pixel's column is fixed);
+//    pixels touch, at a pitch WPM >= W + px whose tail columns stay zero, rows above / below the
+//    image zero (OOB misses), filled by LDS-DMA of row runs (16-B pieces when W % 4 == 0): every
+//    input element of the strip is fetched once per tile, not once per filter tap (KY*KX times);
+//  * the f32 MFMA runs on the vector datapath, so every other vector instruction of a step is
+//    MFMA time lost (PMC + diagnostic builds, profiles/r02): a step is MFMAs plus one vector
+//    LDS read per fragment at compile-time offsets -- no address arithmetic, no edge selects (a
+//    tap left / right of the image reads a zero tail column or the zero guard);
 //  * a tile is OCT = 32*TM output channels x NPX = 128*TN consecutive output pixels of the
 //    flattened (image, oy, ox) space -- tiles run across image boundaries, so small images
 //    (13x13, 7x7) waste no MFMA rows. The strip's rows are "virtual" padded input rows
@@ -38,26 +39,36 @@ __device__ __forceinline__ uint32_t dcm_lb(uint32_t bid, uint32_t G) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int KY, int KX, int SL, int CI, int TM, int TN, int D>
-__global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
-  constexpr int NW = 4, NT = 256;
-  constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
+// Strip: [CI][RIN][WPM], WPM >= W + px; columns W .. WPM-1 of every row stay zero (misses), so a
+// tap left of the image wraps into the previous row's zero tail (a zero guard precedes the strip
+// for its first row) and a tap right of it reads this row's tail: no per-step select. V4: rows in
+// 16-B pieces (W % 4 == 0), else dword elements.
+// WO wave groups of 4 along the output channels (WO = 2: 8 waves, two per SIMD, sharing one
+// stage); a wave owns 32*TN pixels (wave % 4) x 32*TM output channels (group wave / 4).
+// DBG (diagnostic builds only, see dcm_cfgs): bit 0 = no DMA after the prologue, bit 1 = no MFMA,
+// bit 3 = no LDS fragment reads
+template <int KY, int KX, int WPM, int RIN, int V4, int CI, int TM, int TN, int WO, int D, int DBG = 0>
+__global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
+  constexpr int NW = 4 * WO, NT = 64 * NW;
+  constexpr int NPX = 4 * 32 * TN, OCT = 32 * TM * WO;
   constexpr int KK = KY * KX, CH2 = CI / 2, STEPS = CH2 * KK;
   constexpr int WPC = CI * KK * OCT / 4;                 // 16-B weight pieces per stage
   constexpr int LWA = (WPC + NW * 64 - 1) / (NW * 64);   // weight DMA instructions per wave
   constexpr int WREG = LWA * NW * 256;                   // floats
-  // one channel's strip: RIN x WPM floats at run time (p.ldc = RIN * WPM <= SL, p.ldb = WPM,
-  // WPM % 4 == 0), loaded in 16-B pieces
-  static_assert(SL % 4 == 0, "16-B strip pieces");
-  constexpr int LWB = (CI * SL / 4 + NW * 64 - 1) / (NW * 64);
-  constexpr int SREG = LWB * NW * 256;
+  constexpr int SLICE = RIN * WPM;                       // one channel's strip
+  static_assert(WPM % 4 == 0, "16-B aligned rows");
+  constexpr int PW = V4 ? 4 : 1;                         // floats per strip DMA lane
+  constexpr int LWB = (CI * SLICE / PW + NW * 64 - 1) / (NW * 64);
+  constexpr int SREG = LWB * NW * 64 * PW;
   constexpr int BREG = NW * 64;                          // the tile's biases, one DMA per wave
-  constexpr int SLOT = WREG + SREG + BREG;
+  constexpr int GZ = 4;                                  // zero guard before the strip
+  constexpr int SLOT = WREG + GZ + SREG + BREG;
   constexpr int LW = LWA + LWB + 1;
   static_assert(CI % 2 == 0, "channel halves");
   static_assert(D >= 2 && (D - 2) * LW <= 63, "vmcnt range");
   static_assert(OCT % 4 == 0 && OCT <= BREG, "16-B weight pieces, biases of one tile");
-  constexpr int PF = TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3);  // LDS fragment prefetch (steps)
+  constexpr int PF = TM * TN >= 4 ? 2 : 3;  // LDS fragment prefetch (steps)
+  static_assert(TM == 1 || TM == 2 || TM == 4, "weight fragments: one b32 / b64 / b128 read");
   constexpr int IS = STEPS > 3 ? STEPS / 2 : 1;                   // steps the next stage's DMAs spread over
   constexpr int NQ = TM * TN * 4;                                 // float4 pieces of a lane's accumulators
 
@@ -68,12 +79,15 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = lane >> 5, li = lane & 31;
+  const int wp = wave & 3, wo = wave >> 2;  // pixel group, output-channel group
   KT(0);
 
   const uint32_t lb = dcm_lb(blockIdx.x, gridDim.x);
   const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
   const uint32_t Hp = p.H + 2 * p.py;
-  const uint32_t WPM = p.ldb, SLICE = p.ldc;
+  // the strip guards stay zero (no DMA targets them); the first stage's barrier orders these
+  // writes before any read
+  if (tid < D * GZ) smem[(tid / GZ) * SLOT + WREG + tid % GZ] = 0.0f;
 
   // tile t: OC tile fastest (consecutive tiles share the input strip through L2)
   auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &n0) {
@@ -101,16 +115,16 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
     wc4[j] = row < (uint32_t)(CI * KK) ? 4 * c4 : 0xffffu;
     wrel[j] = ((tap * p.IC + c) * p.lda + 4 * c4) * 4u;
   }
-  // strip piece e of the [CI][RIN][WPM] image: channel c, strip row r, input columns 4*x4 ..
-  // 4*x4 + 3 (a piece's tail past the row end reads the next row: only masked taps read it)
+  // strip DMA lane e of the [CI][RIN][WPM] image: channel c, strip row r, input columns x ..
+  // x + PW - 1 (columns at or past W: never loaded, zero)
   uint32_t sr[LWB], sx[LWB];  // sx = channel offset + input column, or 0xffffffff (never loads)
 #pragma unroll
   for (int j = 0; j < LWB; ++j) {
     const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
-    const uint32_t c = e / (SLICE / 4), rem = e - c * (SLICE / 4);
-    const uint32_t r = rem / (WPM / 4), x4 = rem - r * (WPM / 4);
+    const uint32_t c = e / (SLICE / PW), rem = e % (SLICE / PW);
+    const uint32_t r = rem / (WPM / PW), x = (rem % (WPM / PW)) * PW;
     sr[j] = r;
-    sx[j] = c < (uint32_t)CI ? c * p.HW + 4 * x4 : 0xffffffffu;
+    sx[j] = ((c < (uint32_t)CI) & (x < p.W)) ? c * p.HW + x : 0xffffffffu;
   }
   // the strip offsets of the tile being issued (channel 0 of the stage; OOB where the element
   // is padding or past the images), recomputed only when the issue side enters a new tile
@@ -150,50 +164,65 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
   auto issue_one = [&](int q, int slot, uint32_t vo) {
     float *const base = smem + slot * SLOT;
     if (q < LWA) dma16(rsw, base + (wave * LWA + q) * 256, vo);
-    else if (q < LWA + LWB) dma16(rsi, base + WREG + (wave * LWB + q - LWA) * 256, vo);
-    else dma4(rsbias, base + WREG + SREG + 64 * wave, vo);
+    else if (q < LWA + LWB) {
+      if constexpr (V4) dma16(rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 256, vo);
+      else dma4(rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 64, vo);
+    }
+    else dma4(rsbias, base + WREG + GZ + SREG + 64 * wave, vo);
   };
 
   f32x16 acc[TM][TN];
   uint32_t poff[TN];  // this lane's pixels' strip offsets in the current tile (bytes), half included
-  uint32_t xin[TN];   // bit kx: the pixel's tap column kx is inside the image
 
   // one stage = CI channels of one tile: STEPS steps of TM x TN MFMAs; iteration it_issue's DMAs
   // go out over the first IS steps; LDS fragments are read PF steps ahead
   auto compute = [&](int slot, int islot, uint32_t it_issue) {
     uint32_t vo[LW];
     plan(it_issue, vo);
-    const float *const Ab = smem + slot * SLOT + kh * (CH2 * KK * OCT) + li;
-    const char *const Sb = (const char *)(smem + slot * SLOT + WREG);
-    auto frag = [&](int s, float (&a)[TM], float (&b)[TN]) {
+    // a lane's TM weight columns are adjacent (MFMA tile t, lane li: output channel TM*li + t of
+    // the wave's group): one ds_read_b64 / b128 per step instead of TM ds_read_b32 (b32 reads
+    // reach their rate only at ~4 waves per SIMD)
+    const float *const Ab = smem + slot * SLOT + kh * (CH2 * KK * OCT) + wo * 32 * TM + TM * li;
+    const char *const Sb = (const char *)(smem + slot * SLOT + WREG + GZ);
+    auto frag = [&](int s, typename fvec<TM>::t &a, float (&b)[TN]) {
       const int cc = s / KK, tap = s % KK;
+      if constexpr ((DBG & 8) != 0) {  // diagnostic build: no LDS fragment reads
+        a = typename fvec<TM>::t{};
 #pragma unroll
-      for (int t = 0; t < TM; ++t) a[t] = Ab[(cc * KK + tap) * OCT + 32 * t];
-      // row base (run-time pitch) + the tap's column as an immediate offset
-      const uint32_t ro = (uint32_t)cc * SLICE * 4u + (uint32_t)(tap / KX) * WPM * 4u;
+        for (int tn = 0; tn < TN; ++tn) b[tn] = (float)(s + tn);
+        return;
+      }
+      a = *(const typename fvec<TM>::t *)&Ab[(cc * KK + tap) * OCT];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(Sb + (poff[tn] + ro) + (tap % KX) * 4);
+      for (int tn = 0; tn < TN; ++tn)
+        b[tn] = *(const float *)(Sb + poff[tn] + (cc * SLICE + (tap / KX) * WPM + tap % KX) * 4);
     };
-    float a[PF + 1][TM], b[PF + 1][TN];
+    typename fvec<TM>::t a[PF + 1];
+    float b[PF + 1][TN];
 #pragma unroll
     for (int s = 0; s < PF; ++s) frag(s, a[s], b[s]);
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
       if (s + PF < STEPS) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
-      // taps left / right of the image read a neighbouring element: zero them here, at the
-      // use (a select next to the load would make the prefetch wait for the LDS latency)
-      float bm[TN];
+      const float *const bm = b[s % (PF + 1)];
+      if constexpr ((DBG & 2) != 0) {  // diagnostic build: no MFMA (the fragments are still consumed)
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) bm[tn] = (xin[tn] >> ((s % KK) % KX)) & 1u ? b[s % (PF + 1)][tn] : 0.0f;
+        for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int t = 0; t < TM; ++t)
+          for (int tn = 0; tn < TN; ++tn) acc[t][tn][0] += bm[tn] * vget<TM>(a[s % (PF + 1)], t);
+      } else {
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(bm[tn], a[s % (PF + 1)][t], acc[t][tn], 0, 0, 0);
+        for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
-        issue_one(q, islot, vo[q]);
+          for (int tn = 0; tn < TN; ++tn)
+            acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(bm[tn], vget<TM>(a[s % (PF + 1)], t), acc[t][tn], 0, 0, 0);
+      }
+      if constexpr ((DBG & 1) == 0) {  // diagnostic build 1: no DMA after the prologue
+#pragma unroll
+        for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
+          issue_one(q, islot, vo[q]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -203,18 +232,18 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
   const bool vec = p.cvec != 0 && !p.res;  // float4 pixel quads (OHW % 4 == 0: a quad is in one image)
 
   // bias, residual, ReLU and store of a tile's values: v[q], q = (t, tn, gq) holds output channel
-  // oc0 + 32 t + li, pixels n0 + wave*32*TN + 32 tn + 8 gq + 4 kh + e (e = 0..3)
+  // oc0 + wo*32*TM + TM*li + t, pixels n0 + wp*32*TN + 32 tn + 8 gq + 4 kh + e (e = 0..3)
   auto store_tile = [&](uint32_t oc0, uint32_t n0, const float *Lb, f32x4v (&v)[NQ]) {
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
-      const uint32_t m = oc0 + 32 * t + li;
-      const float bb = Lb[32 * t + li];
+      const uint32_t m = oc0 + (uint32_t)(wo * 32 * TM + TM * li + t);
+      const float bb = Lb[wo * 32 * TM + TM * li + t];
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           f32x4v x = v[(t * TN + tn) * 4 + gq];
-          const uint32_t nq = n0 + (uint32_t)(wave * 32 * TN + 32 * tn + 8 * gq + 4 * kh);
+          const uint32_t nq = n0 + (uint32_t)(wp * 32 * TN + 32 * tn + 8 * gq + 4 * kh);
           if (vec) {
             const uint32_t img = fdiv(nq, p.ohw_m, p.ohw_s);
             const uint32_t o = oob_unless((m < p.M) & (nq < p.N), (img * p.OCOHW + m * p.OHW + nq - img * p.OHW) * 4u);
@@ -246,7 +275,7 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
   auto finish_tile = [&](uint32_t t, int cslot) {
     uint32_t oc0, n0;
     tile_of(t, oc0, n0);
-    const float *const Lb = smem + cslot * SLOT + WREG + SREG;
+    const float *const Lb = smem + cslot * SLOT + WREG + GZ + SREG;
     f32x4v v[NQ];
 #pragma unroll
     for (int t2 = 0; t2 < TM; ++t2)
@@ -317,18 +346,13 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
     const uint32_t v0 = vrow0(n0);
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const uint32_t n = n0 + (uint32_t)(wave * 32 * TN + 32 * tn + li);
+      const uint32_t n = n0 + (uint32_t)(wp * 32 * TN + 32 * tn + li);
       const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
       const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
       // pixels past the op read strip position 0 (their results are dropped)
-      // (ox - px may be negative: the strip follows the weight region, so such an address is
-      // still inside the slot; the tap is masked)
+      // (ox - px may be negative: the guard / the previous row's zero tail)
       poff[tn] = n < p.N ? ((img * Hp + oy - v0) * WPM + ox - p.px) * 4u : 0u;
       poff[tn] += (uint32_t)kh * CH2 * SLICE * 4u;
-      uint32_t m = 0;
-#pragma unroll
-      for (int kx = 0; kx < KX; ++kx) m |= ((ox + (uint32_t)kx - p.px) < p.W ? 1u : 0u) << kx;
-      xin[tn] = m;
     }
 #pragma unroll
     for (int t2 = 0; t2 < TM; ++t2)
@@ -338,7 +362,7 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
         for (int r = 0; r < 16; ++r) acc[t2][tn][r] = 0.0f;
     int cslot = 0;
     for (; it < iend; ++it) {
-      vm_wait<(D - 2) * LW>();
+      vm_wait<(DBG & 1) ? 0 : (D - 2) * LW>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage it landed for all waves; all done reading it-1
       asm volatile("" ::: "memory");
@@ -356,16 +380,16 @@ __global__ __launch_bounds__(256) void dcm_kernel(GemmArgs p) {
 #endif
 }
 
-template <int KY, int KX, int SL, int CI, int TM, int TN, int D>
+template <int KY, int KX, int WPM, int RIN, int V4, int CI, int TM, int TN, int WO, int D, int DBG = 0>
 cfg_t dcm_cfg(const char *name) {
-  cfg_t c{name, 32 * TM, 128 * TN, CI * KY * KX, 256, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dcm_kernel<KY, KX, SL, CI, TM, TN, D>;
+  cfg_t c{name, 32 * TM * WO, 128 * TN, CI * KY * KX, 256 * WO, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = dcm_kernel<KY, KX, WPM, RIN, V4, CI, TM, TN, WO, D, DBG>;
   c.dc = 2;
   c.dc_ky = KY;
   c.dc_kx = KX;
-  c.dc_s = 1;
-  c.dc_wpm = SL;  // strip floats per channel (rows x run-time pitch)
-  c.dc_rin = 0;
+  c.dc_s = V4;  // dcm: 16-B strip pieces (rows of W % 4 == 0)
+  c.dc_wpm = WPM;
+  c.dc_rin = RIN;
   c.dc_ci = CI;
   return c;
 }
@@ -373,22 +397,36 @@ cfg_t dcm_cfg(const char *name) {
 }  // namespace
 
 std::vector<cfg_t> dcm_cfgs() {
+  // <KY, KX, WPM, RIN, V4, CI, TM, TN, WO, D>: strip pitch / rows by input width class; x64 tiles
+  // fit two blocks per CU, w8 (two wave groups) puts two waves per SIMD on one 128-channel stage
   return {
-      // 3x3. Strip capacity per channel (rows x pitch): 256 floats: 13x13 / 14x14 (16 x <= 15
-      // rows), 28x28 (28 x 9); 448: 56x56 (56 x 8), 6x6 / 7x7 (8 x <= 41 rows over 4-5 images).
-      // Most fit two blocks per CU (<= 80 KB): two waves per SIMD hide each other's barrier,
-      // LDS-latency and DMA-issue stalls, which one wave per SIMD leaves as MFMA idle time.
-      dcm_cfg<3, 3, 256, 8, 4, 1, 3>("dm3s256x128c8"),
-      dcm_cfg<3, 3, 256, 8, 2, 1, 2>("dm3s256x64c8"),
-      dcm_cfg<3, 3, 256, 8, 3, 1, 2>("dm3s256x96c8"),
-      dcm_cfg<3, 3, 256, 4, 4, 1, 3>("dm3s256x128c4"),
-      dcm_cfg<3, 3, 448, 8, 2, 1, 2>("dm3s448x64c8"),
-      dcm_cfg<3, 3, 448, 4, 4, 1, 2>("dm3s448x128c4"),
-      dcm_cfg<3, 3, 448, 4, 3, 1, 3>("dm3s448x96c4"),
-      // 5x5: 27x27 / 28x28 (28 x <= 14 rows), 14x14 (16 x <= 19)
-      dcm_cfg<5, 5, 400, 4, 4, 1, 2>("dm5s400x128c4"),
-      dcm_cfg<5, 5, 400, 4, 2, 1, 2>("dm5s400x64c4"),
-      dcm_cfg<5, 5, 400, 2, 4, 1, 3>("dm5s400x128c2"),
+      // 3x3 p1: 13x13 / 14x14 (pitch 16, <= 16 rows), 6x6 / 7x7 (8, <= 44 rows over 4-5 images),
+      // 28x28 (32, 16-B pieces), 56x56 (60, 16-B pieces)
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2>("dm3w16x64c8"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 2, 3>("dm3w16x128c8w8"),
+      dcm_cfg<3, 3, 16, 16, 0, 4, 4, 1, 1, 3>("dm3w16x128c4"),
+      dcm_cfg<3, 3, 8, 44, 0, 8, 2, 1, 1, 2>("dm3w8x64c8"),
+      dcm_cfg<3, 3, 8, 44, 0, 8, 2, 1, 2, 2>("dm3w8x128c8w8"),
+      dcm_cfg<3, 3, 32, 10, 1, 8, 2, 1, 1, 2>("dm3w32x64c8"),
+      dcm_cfg<3, 3, 32, 10, 1, 8, 2, 1, 2, 2>("dm3w32x128c8w8"),
+      dcm_cfg<3, 3, 60, 8, 1, 8, 2, 1, 1, 2>("dm3w60x64c8"),
+      dcm_cfg<3, 3, 60, 8, 1, 8, 2, 1, 2, 2>("dm3w60x128c8w8"),
+      dcm_cfg<3, 3, 60, 8, 1, 4, 2, 1, 1, 3>("dm3w60x64c4"),
+      // 5x5 p2: 27x27 (pitch 32, dword), 28x28 (32, 16-B pieces), 14x14 (16, <= 20 rows)
+      dcm_cfg<5, 5, 32, 14, 0, 4, 2, 1, 1, 2>("dm5w32x64c4"),
+      dcm_cfg<5, 5, 32, 14, 0, 4, 2, 1, 2, 2>("dm5w32x128c4w8"),
+      dcm_cfg<5, 5, 32, 14, 1, 4, 2, 1, 1, 2>("dm5w32vx64c4"),
+      dcm_cfg<5, 5, 16, 20, 0, 4, 2, 1, 1, 2>("dm5w16x64c4"),
+#ifdef BH_KTRACE
+      // diagnostic builds (instrumented library only; wrong results by design)
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 1>("xdm3w16x64c8_nodma"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 2>("xdm3w16x64c8_nomfma"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 3>("xdm3w16x64c8_none"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 2, 3, 1>("xdm3w16x128c8w8_nodma"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 2, 3, 2>("xdm3w16x128c8w8_nomfma"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 9>("xdm3w16x64c8_nodma_noread"),
+      dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 8>("xdm3w16x64c8_noread"),
+#endif
   };
 }
 
@@ -399,14 +437,14 @@ std::vector<cfg_t> dcm_cfgs() {
 // per block.
 int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
                uint32_t sx, uint32_t splits, bool first) {
-  if ((int)KY != c.dc_ky || (int)KX != c.dc_kx || sy != 1 || sx != 1)
+  if ((int)KY != c.dc_ky || (int)KX != c.dc_kx || sy != 1 || sx != 1 || p.py >= KY)
     return bh::fail(BH_UNSUP, std::string("conv: direct config ") + c.name + " is for another kernel / stride");
   if (p.IC % (uint32_t)c.dc_ci)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a multiple of ") + c.name + "'s group");
   const uint32_t npx = (uint32_t)c.BN, OW = p.OW, OHW = p.OHW, Hp = p.H + 2 * p.py;
-  // strip pitch: the input row rounded up to 16-B pieces (no horizontal padding: masked taps)
-  if (p.px >= (uint32_t)c.dc_kx) return bh::fail(BH_UNSUP, "conv: horizontal padding of a whole kernel");
-  const uint32_t wpm = (p.W + 3) & ~3u;
+  // strip pitch: the row plus a zero tail wide enough for the horizontal padding
+  if (p.W + p.px > (uint32_t)c.dc_wpm || p.px > 4 || (c.dc_s && p.W % 4))
+    return bh::fail(BH_UNSUP, std::string("conv: input rows do not fit the strip of ") + c.name);
   const uint32_t ptiles = (p.N + npx - 1) / npx;
   // strip rows the worst pixel tile touches (virtual padded rows img*Hp + oy .. + KY - 1)
   uint32_t rin = 0;
@@ -415,10 +453,8 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
     const uint32_t va = (a / OHW) * Hp + (a % OHW) / OW, vb = (b / OHW) * Hp + (b % OHW) / OW;
     rin = std::max(rin, vb - va + KY);
   }
-  if ((uint64_t)rin * wpm > (uint64_t)c.dc_wpm)
+  if (rin > (uint32_t)c.dc_rin)
     return bh::fail(BH_UNSUP, std::string("conv: pixel tile's input strip too large for ") + c.name);
-  p.ldb = wpm;
-  p.ldc = rin * wpm;
   const uint64_t out_bytes = (uint64_t)B * p.OCOHW * 4;
   if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the direct kernel");
   p.c_bytes = (uint32_t)out_bytes;
@@ -428,7 +464,7 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   if (total >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many iterations");
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256, 0) != hipSuccess || occ < 1) occ = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, c.NT, 0) != hipSuccess || occ < 1) occ = 1;
   const bool whole = splits > 4;
   uint32_t bpc = splits ? (whole ? splits - 4 : splits) : 2;
   bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
@@ -451,8 +487,7 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   f = bh::make_fastdiv(Hp);
   p.kyx_m = f.m;
   p.kyx_s = f.s;
-  const uint32_t NQ4 = (uint32_t)(c.BM / 32) * (uint32_t)(c.BN / 128) * 4;  // float4 pieces per lane
-  int rc = ensure_ws(ctx, (size_t)2 * G * NQ4 * 256 * 16);
+  int rc = ensure_ws(ctx, (size_t)2 * G * c.BM * c.BN * 4);  // two tile slabs per block
   if (rc == BH_OK) rc = ensure_cnt(ctx, (size_t)ntile);
   if (rc != BH_OK) return rc;
   p.ws = (float *)ctx->ws;
@@ -461,7 +496,7 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   p.trace = (unsigned long long *)ctx->stamps + 65536;
 #endif
   void *args[] = {&p};
-  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(256), args, first, true, "conv_direct_mc");
+  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(c.NT), args, first, true, "conv_direct_mc");
 }
 
 }  // namespace bhk

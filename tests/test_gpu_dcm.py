@@ -89,7 +89,7 @@ def test_dm_rejects_other_kernels(dev, cn):
         dev.tune_set(1, -1, 0)
 
 
-@pytest.mark.parametrize("cn", [n for n in DM if n in ("dm3s256x96c8", "dm5s400x64c4")])
+@pytest.mark.parametrize("cn", [n for n in DM if n in ("dm3w16x64c8", "dm5w32x64c4")])
 def test_dm_residual_and_slab(dev, cn):
     s = SHAPES[kernel_of(cn)][0]
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
