@@ -11,6 +11,8 @@ import statistics
 import sys
 
 out_dir, bench_json, dest = sys.argv[1], sys.argv[2], sys.argv[3]
+# the hot-path kernels (gen_data, stamps, runtime fills / copies, repacks and reduce passes excluded)
+MAIN = ("gemm_kernel", "ring_kernel", "srk_kernel", "gv_kernel", "dc_kernel", "dcm_kernel")
 b = json.loads([l for l in open(bench_json) if l.startswith("{")][-1])
 per_shape = []
 for d in sorted(glob.glob(os.path.join(out_dir, "shape*"))):
@@ -21,7 +23,7 @@ for d in sorted(glob.glob(os.path.join(out_dir, "shape*"))):
             continue
         per = {}
         for r in csv.DictReader(open(f[0])):
-            if "gemm_kernel" not in r["Kernel_Name"] or r["Counter_Name"] != ctr:
+            if not any(k in r["Kernel_Name"] for k in MAIN) or r["Counter_Name"] != ctr:
                 continue
             per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
         vals[ctr] = statistics.median(per.values()) if per else None
