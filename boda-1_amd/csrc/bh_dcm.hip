@@ -55,7 +55,9 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
   constexpr int WPC = CI * KK * OCT / 4;                 // 16-B weight pieces per stage
   constexpr int LWA = (WPC + NW * 64 - 1) / (NW * 64);   // weight DMA instructions per wave
   constexpr int WREG = LWA * NW * 256;                   // floats
-  constexpr int SLICE = RIN * WPM;                       // one channel's strip
+  // P1 (1x1, no padding): a channel's strip is exactly the tile's NPX pixels, [CI][NPX]
+  constexpr bool P1 = KY == 1 && KX == 1;
+  constexpr int SLICE = P1 ? NPX : RIN * WPM;            // one channel's strip
   static_assert(WPM % 4 == 0, "16-B aligned rows");
   constexpr int PW = V4 ? 4 : 1;                         // floats per strip DMA lane
   constexpr int LWB = (CI * SLICE / PW + NW * 64 - 1) / (NW * 64);
@@ -122,9 +124,14 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
   for (int j = 0; j < LWB; ++j) {
     const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
     const uint32_t c = e / (SLICE / PW), rem = e % (SLICE / PW);
-    const uint32_t r = rem / (WPM / PW), x = (rem % (WPM / PW)) * PW;
-    sr[j] = r;
-    sx[j] = ((c < (uint32_t)CI) & (x < p.W)) ? c * p.HW + x : 0xffffffffu;
+    if constexpr (P1) {  // pixel slot rem*PW of the tile, channel c
+      sr[j] = rem * PW;
+      sx[j] = c < (uint32_t)CI ? c * p.HW : 0xffffffffu;
+    } else {
+      const uint32_t r = rem / (WPM / PW), x = (rem % (WPM / PW)) * PW;
+      sr[j] = r;
+      sx[j] = ((c < (uint32_t)CI) & (x < p.W)) ? c * p.HW + x : 0xffffffffu;
+    }
   }
   // the strip offsets of the tile being issued (channel 0 of the stage; OOB where the element
   // is padding or past the images), recomputed only when the issue side enters a new tile
@@ -143,6 +150,15 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < LWA; ++j) vo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
     if (t != ls_tile) {  // uniform
+      if constexpr (P1) {
+#pragma unroll
+        for (int j = 0; j < LWB; ++j) {
+          // PW pixels from n0 + sr[j]: one image (OHW % PW == 0), past the op: misses
+          const uint32_t n = n0 + sr[j];
+          const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
+          srel[j] = oob_unless((sx[j] != 0xffffffffu) & (n < p.N), (img * p.ICHW + sx[j] + n - img * p.OHW) * 4u);
+        }
+      } else {
       const uint32_t v0 = vrow0(n0);
 #pragma unroll
       for (int j = 0; j < LWB; ++j) {
@@ -151,6 +167,7 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
         const uint32_t iy = vr - img * Hp - p.py;         // wraps (misses) in the top padding
         const bool ok = (sx[j] != 0xffffffffu) & (iy < p.H) & (img < p.tiles_n);  // tiles_n = images
         srel[j] = oob_unless(ok, (img * p.ICHW + iy * p.W + sx[j]) * 4u);
+      }
       }
       ls_tile = t;
     }
@@ -343,10 +360,14 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
     const uint32_t iend = min(it1, (t + 1) * p.ipt);
     uint32_t oc0, n0;
     tile_of(t, oc0, n0);
-    const uint32_t v0 = vrow0(n0);
+    const uint32_t v0 = P1 ? 0u : vrow0(n0);
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const uint32_t n = n0 + (uint32_t)(wp * 32 * TN + 32 * tn + li);
+      if constexpr (P1) {  // the pixel's slot of the tile
+        poff[tn] = (uint32_t)(wp * 32 * TN + 32 * tn + li) * 4u + (uint32_t)kh * CH2 * SLICE * 4u;
+        continue;
+      }
       const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
       const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
       // pixels past the op read strip position 0 (their results are dropped)
@@ -417,6 +438,12 @@ std::vector<cfg_t> dcm_cfgs() {
       dcm_cfg<5, 5, 32, 14, 0, 4, 2, 1, 2, 2>("dm5w32x128c4w8"),
       dcm_cfg<5, 5, 32, 14, 1, 4, 2, 1, 1, 2>("dm5w32vx64c4"),
       dcm_cfg<5, 5, 16, 20, 0, 4, 2, 1, 1, 2>("dm5w16x64c4"),
+      // 1x1: CI channels of the tile's 128 pixels per stage (16-B pieces when OH*OW % 4 == 0)
+      dcm_cfg<1, 1, 0, 0, 1, 32, 2, 1, 1, 3>("dm1vx64c32"),
+      dcm_cfg<1, 1, 0, 0, 1, 32, 2, 1, 2, 3>("dm1vx128c32w8"),
+      dcm_cfg<1, 1, 0, 0, 1, 16, 2, 1, 1, 4>("dm1vx64c16"),
+      dcm_cfg<1, 1, 0, 0, 0, 32, 2, 1, 1, 3>("dm1x64c32"),
+      dcm_cfg<1, 1, 0, 0, 0, 32, 2, 1, 2, 3>("dm1x128c32w8"),
 #ifdef BH_KTRACE
       // diagnostic builds (instrumented library only; wrong results by design)
       dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 1>("xdm3w16x64c8_nodma"),
@@ -442,9 +469,14 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   if (p.IC % (uint32_t)c.dc_ci)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a multiple of ") + c.name + "'s group");
   const uint32_t npx = (uint32_t)c.BN, OW = p.OW, OHW = p.OHW, Hp = p.H + 2 * p.py;
-  // strip pitch: the row plus a zero tail wide enough for the horizontal padding
-  if (p.W + p.px > (uint32_t)c.dc_wpm || p.px > 4 || (c.dc_s && p.W % 4))
+  const bool p1 = KY == 1 && KX == 1;
+  if (p1) {  // 1x1: strip = the tile's pixels; 16-B pieces need quads inside one image
+    if (p.py || p.px || (c.dc_s && OHW % 4))
+      return bh::fail(BH_UNSUP, std::string("conv: padded 1x1 / pixel quads across images for ") + c.name);
+  } else if (p.W + p.px > (uint32_t)c.dc_wpm || p.px > 4 || (c.dc_s && p.W % 4)) {
+    // strip pitch: the row plus a zero tail wide enough for the horizontal padding
     return bh::fail(BH_UNSUP, std::string("conv: input rows do not fit the strip of ") + c.name);
+  }
   const uint32_t ptiles = (p.N + npx - 1) / npx;
   // strip rows the worst pixel tile touches (virtual padded rows img*Hp + oy .. + KY - 1)
   uint32_t rin = 0;
@@ -453,7 +485,7 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
     const uint32_t va = (a / OHW) * Hp + (a % OHW) / OW, vb = (b / OHW) * Hp + (b % OHW) / OW;
     rin = std::max(rin, vb - va + KY);
   }
-  if (rin > (uint32_t)c.dc_rin)
+  if (!p1 && rin > (uint32_t)c.dc_rin)
     return bh::fail(BH_UNSUP, std::string("conv: pixel tile's input strip too large for ") + c.name);
   const uint64_t out_bytes = (uint64_t)B * p.OCOHW * 4;
   if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the direct kernel");

@@ -196,8 +196,8 @@ __device__ __forceinline__ void combine_store(const GemmArgs &p, uint32_t tile, 
 
 // In-kernel split-K combine of a whole tile by one block (the last arriver): each
 // thread owns CH float4 chunks (c = tid + j*NT), processed G at a time with all of
-// a group's loads for two slabs issued before any is consumed, so the slab reads
-// overlap instead of costing one L2 round trip per chunk. Same fixed slab order as
+// a group's loads for four slabs issued before any is consumed, so the slab reads
+// overlap instead of costing one round trip per chunk and slab. Same fixed slab order as
 // combine_store (bitwise identical results).
 template <int IMODE, int NT, int CH, int G, int NCH = CH * NT>
 __device__ __forceinline__ void combine_tile(const GemmArgs &p, uint32_t tile, uint32_t tile_m, uint32_t tile_n,
@@ -215,25 +215,22 @@ __device__ __forceinline__ void combine_tile(const GemmArgs &p, uint32_t tile, u
       off[j] = (tile * tsz + 4 * (uint32_t)(tid + (g + j) * NT)) * 4;
       sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    uint32_t q = 0;
-    for (; q + 2 <= S; q += 2) {
-      f32x4v x0[G], x1[G];
+    // four slabs per round trip (the last round's missing slabs read OOB zeros and are not
+    // added: the sum is the same sequence of additions as combine_store's)
+    for (uint32_t q = 0; q < S; q += 4) {
+      f32x4v x[4][G];
 #pragma unroll
-      for (int j = 0; j < G; ++j) {
-        x0[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
-        x1[j] = __builtin_bit_cast(f32x4v,
-                                   __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + (q + 1) * sstep, 0, AUX_SC1));
-      }
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < G; ++j) {
-        sum[j] += x0[j];
-        sum[j] += x1[j];
-      }
-    }
-    if (q < S) {
+        for (int j = 0; j < G; ++j)
+          x[i][j] = __builtin_bit_cast(
+              f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, oob_unless(q + i < S, off[j] + (q + i) * sstep), 0,
+                                                            AUX_SC1));
 #pragma unroll
-      for (int j = 0; j < G; ++j)
-        sum[j] += __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rw, off[j] + q * sstep, 0, AUX_SC1));
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+          if (q + i < S) sum[j] += x[i][j];
     }
 #pragma unroll
     for (int j = 0; j < G; ++j) finish_store<IMODE>(p, tile_m, tile_n, (uint32_t)(tid + (g + j) * NT), sum[j], bias_lds);

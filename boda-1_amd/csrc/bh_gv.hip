@@ -224,14 +224,23 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
   f32x4v sum[CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t q = 0; q < gridDim.y; ++q) {
-    f32x4v x[CH];
+  // four K chunks per round trip (missing ones read OOB zeros and are not added: same order)
+  const uint32_t S = gridDim.y;
+  for (uint32_t q = 0; q < S; q += 4) {
+    f32x4v x[4][CH];
 #pragma unroll
-    for (int j = 0; j < CH; ++j)
-      x[j] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rall, q * tstep + (tile * TSZ + 4 * (uint32_t)(tid + j * NT)) * 4, 0, AUX_SC1));
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < CH; ++j) sum[j] += x[j];
+      for (int j = 0; j < CH; ++j)
+        x[i][j] = __builtin_bit_cast(
+            f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                        rall, oob_unless(q + i < S, (q + i) * tstep + (tile * TSZ + 4 * (uint32_t)(tid + j * NT)) * 4), 0,
+                        AUX_SC1));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (q + i < S) sum[j] += x[i][j];
   }
 #pragma unroll
   for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);

@@ -35,6 +35,11 @@ SHAPES = {
         ops.ConvShape(1, 16, 27, 30, 64, 3, 3, 1, 1, 1, 1),
         ops.ConvShape(2, 16, 56, 56, 64, 3, 3, 1, 1, 1, 1),
         ops.ConvShape(1, 24, 40, 62, 50, 3, 3, 1, 1, 1, 1)],
+    1: [ops.ConvShape(2, 64, 14, 14, 96, 1, 1, 1, 1, 0, 0),    # 16-B quads (OH*OW % 4 == 0)
+        ops.ConvShape(3, 32, 13, 13, 70, 1, 1, 1, 1, 0, 0),    # dword (169 pixels per image)
+        ops.ConvShape(1, 96, 28, 28, 130, 1, 1, 1, 1, 0, 0),
+        ops.ConvShape(5, 160, 6, 6, 64, 1, 1, 1, 1, 0, 0),
+        ops.ConvShape(2, 32, 7, 9, 40, 1, 1, 1, 1, 0, 0)],
     5: [ops.ConvShape(2, 32, 27, 27, 64, 5, 5, 1, 1, 2, 2),
         ops.ConvShape(1, 8, 28, 28, 40, 5, 5, 1, 1, 2, 2),
         ops.ConvShape(2, 12, 14, 14, 20, 5, 5, 1, 1, 2, 2),
@@ -80,11 +85,12 @@ def test_dm_rejects_other_kernels(dev, cn):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
     try:
         with pytest.raises(boda_hip.UnsupportedError):
-            run_conv(dev, ops.ConvShape(1, 16, 30, 30, 16, 7, 7, 1, 1, 3, 3))
+            run_conv(dev, ops.ConvShape(1, 32, 30, 30, 16, 7, 7, 1, 1, 3, 3))
         with pytest.raises(boda_hip.UnsupportedError):  # stride 2
             run_conv(dev, ops.ConvShape(1, 16, 13, 13, 16, kernel_of(cn), kernel_of(cn), 2, 2, 1, 1))
+        k = kernel_of(cn)
         with pytest.raises(boda_hip.UnsupportedError):  # 3 input channels: not a multiple of any group
-            run_conv(dev, ops.ConvShape(1, 3, 13, 13, 16, kernel_of(cn), kernel_of(cn), 1, 1, 1, 1))
+            run_conv(dev, ops.ConvShape(1, 3, 13, 13, 16, k, k, 1, 1, k // 2, k // 2))
     finally:
         dev.tune_set(1, -1, 0)
 
