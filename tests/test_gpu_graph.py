@@ -61,3 +61,93 @@ def test_time_next_call_covers_split_k_reduce(dev):
     finally:
         dev.tune_set(1, -1, 0)
         wl.free()
+
+
+def _cfg(name):
+    import boda_hip
+    return boda_hip.tune_cfg_names(1).index(name)
+
+
+def test_workspace_growth_under_capture_is_a_named_error():
+    """A split-K call whose workspace must grow while the stream is being captured fails with a
+    named error (bh_ctx workspaces never reallocate inside a capture), not a HIP capture fault."""
+    import boda_hip
+    d = boda_hip.Device(0)  # fresh context: empty workspaces
+    s = ops.ConvShape(1, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)
+    wl = runner.Workload(d, [s])
+    d.tune_set(1, _cfg("r64x64x32d3"), 4)
+    try:
+        d.capture_begin()
+        with pytest.raises(RuntimeError, match="captured"):
+            wl.launch(0)
+        try:
+            d.capture_end()
+        except RuntimeError:
+            pass  # the aborted capture may be invalidated; what matters is the named error above
+        d.sync()
+        wl.launch(0)  # eager: grows the workspace; a capture now succeeds
+        d.capture_begin()
+        wl.launch(0)
+        d.graph_destroy(d.capture_end())
+    finally:
+        d.tune_set(1, -1, 0)
+        wl.free()
+        d.close()
+
+
+def test_graph_survives_workspace_growth():
+    """A graph captured with a small split-K op keeps its (retired, not freed) workspace after a
+    bigger split-K op grows the context's workspace eagerly: its replay is bit-exact."""
+    import boda_hip
+    d = boda_hip.Device(0)
+    small = ops.ConvShape(1, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)
+    big = ops.ConvShape(20, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)
+    ws = runner.Workload(d, [small])
+    wb = runner.Workload(d, [big])
+    d.tune_set(1, _cfg("r64x64x32d3"), 4)
+    try:
+        ws.launch(0)
+        d.sync()
+        ref = ws.output(0)
+        ws.ops[0].bufs[-1].zero()
+        g = ws.capture_step()
+        wb.launch(0)  # grows the workspace (the small op's buffer is retired, the graph holds it)
+        d.sync()
+        d.graph_launch(g)
+        d.graph_launch(g)
+        d.sync()
+        np.testing.assert_array_equal(ws.output(0), ref)
+        d.graph_destroy(g)
+    finally:
+        d.tune_set(1, -1, 0)
+        ws.free()
+        wb.free()
+        d.close()
+
+
+def test_armed_events_cleared_by_a_failed_call(dev):
+    """bh_time_next_call arms an event pair for the next call; a call that fails validation
+    before launching clears it, so the pair never attaches to a later, unrelated launch (here a
+    ~1 ms SGEMM: had the pair attached to it, it would time ~1 ms)."""
+    import boda_hip
+    s = ops.SgemmShape(4096, 4096, 4096)
+    wl = runner.Workload(dev, [s])
+    a, b, c = wl.ops[0].bufs
+    wl.launch(0)
+    b0, e0 = dev.time_next_call()
+    wl.launch(0)
+    dev.sync()
+    t_big = dev.elapsed_ms(b0, e0)
+    assert t_big > 0.3
+    b_ev, e_ev = dev.time_next_call()
+    with pytest.raises(boda_hip.UnsupportedError):
+        dev.sgemm(a, b, c, 0, 4096, 4096)  # zero-sized: rejected before any launch
+    wl.launch(0)
+    dev.sync()
+    try:
+        t = dev.elapsed_ms(b_ev, e_ev)  # never recorded: an error, or no span at all
+    except RuntimeError:
+        t = 0.0
+    assert t < 0.1 * t_big
+    dev.events_reset()
+    wl.free()
