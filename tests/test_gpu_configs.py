@@ -139,6 +139,10 @@ GV_SHAPES = [
     ops.ConvShape(2, 12, 5, 5, 33, 3, 3, 2, 2, 0, 0),     # stride 2, 8 columns
     ops.ConvShape(2, 48, 14, 14, 70, 3, 3, 1, 1, 1, 1),   # 392 columns: a 2-D tile grid
     ops.ConvShape(1, 200, 7, 7, 40, 1, 1, 1, 1, 0, 0),    # 1x1, 49 columns, K % 16 != 0
+    # im2col gathers: tabulated (B_IMTAB) when a K chunk fits the table and KYX <= 31
+    ops.ConvShape(2, 16, 7, 7, 40, 5, 5, 1, 1, 2, 2),     # 5x5 pad 2: 25 taps
+    ops.ConvShape(1, 256, 5, 5, 24, 3, 3, 1, 1, 1, 1),    # K 2304: past small tables unless split
+    ops.ConvShape(1, 8, 9, 9, 20, 7, 7, 1, 1, 3, 3),      # 49 taps: direct (untabulated) gathers
 ]
 
 
