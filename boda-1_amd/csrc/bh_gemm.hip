@@ -1165,7 +1165,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
   if (no_dc && cfgs(1)[ch.cfg].dc) ch = heuristic(1, d, true, false);
-  if (cfgs(1)[ch.cfg].gv) {
+  if (cfgs(1)[ch.cfg].gv && !cfgs(1)[ch.cfg].packA) {
     // few output columns: stream the bank in its reference layout; the window covering the
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
     const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
@@ -1202,6 +1202,12 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
         if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
         return launch_conv(ctx, in, filts, packed ? packed : wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py,
                            px, relu, out_ctot, res, true);
+      }
+      if (cfgs(1)[ch.cfg].gv) {
+        // register streaming over the packed bank (bh_gv.hip gvp_kernel): 16-deep k groups
+        // inside one filter tap
+        if (IC % 16) return fail(BH_UNSUP, "conv: gvp configs need IC % 16 == 0");
+        return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1S : B_IMTAP, p, "conv", packed != nullptr);
       }
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
       const bool tab = ((p.K + bk - 1) / bk) * bk <= (uint32_t)TAB_MAX;  // K rows a block tabulates

@@ -27,22 +27,139 @@ namespace {
 
 typedef float f32x4t __attribute__((ext_vector_type(4)));
 
+
+// Block geometry of the register-streaming kernels: R x C 16x16 MFMA tiles, NW waves.
+template <int R, int C, int NW>
+struct gv_geom {
+  static constexpr int NT = NW * 64, BMr = 16 * R, NC = 16 * C;
+  static constexpr int TSZ = BMr * NC;  // floats of a block's output tile
+  static constexpr int NCH = TSZ / 4, CH = (NCH + NT - 1) / NT;
+  static_assert(NCH % NT == 0 || NT % NCH == 0, "float4 chunks per thread");
+};
+
+// bias of the rows this thread stores in the epilogue, fetched at kernel entry (a dependent
+// global load at the end of a small op costs a full memory round trip)
+template <int R, int C, int NW>
+__device__ __forceinline__ void gv_bias(const GemmArgs &p, uint32_t m0, int tid, float (&bias_r)[gv_geom<R, C, NW>::CH]) {
+  using G = gv_geom<R, C, NW>;
+  const bool has = G::NCH % G::NT == 0 || tid < G::NCH;
+#pragma unroll
+  for (int j = 0; j < G::CH; ++j) {
+    const uint32_t m = m0 + 4 * (uint32_t)(tid + j * G::NT) / G::NC;
+    bias_r[j] = (has && p.bias && m < p.M) ? p.bias[m] : 0.0f;
+  }
+}
+
+// Epilogue of the register-streaming kernels: the NW waves' partial tiles -> LDS (row-major
+// BMr x NC), summed in wave order; then either stored (one K chunk) or, with K chunks
+// (grid.y > 1), written as this chunk's slab, and the tile's last-arriving block sums the
+// slabs in chunk order (the split-K protocol of bh_gemm.hip: bitwise reproducible).
+// RS: row interleave of the MFMA row tiles -- row rho of tile r is block row RS * rho + r
+// (RS = 1: tile r owns rows 16 r .. 16 r + 15, written as 16 r + rho).
+template <int R, int C, int NW, int RS>
+__device__ __forceinline__ void gv_finish(const GemmArgs &p, f32x4t (&acc)[R][C], float *red, uint32_t tm, uint32_t tn,
+                                          int tid, int wave, int lane,
+                                          const float (&bias_r)[gv_geom<R, C, NW>::CH]) {
+  using G = gv_geom<R, C, NW>;
+  constexpr int NT = G::NT, NC = G::NC, TSZ = G::TSZ, NCH = G::NCH, CH = G::CH;
+  uint32_t *const flag = (uint32_t *)(red + NW * TSZ);
+  const int i = lane & 15, g = lane >> 4;
+  const uint32_t tile = blockIdx.x, split = blockIdx.y;
+  // 16x16x4 C/D map: register j of lane l is row 4 * (l >> 4) + j, column l & 15.
+  {
+    float *const Rw = red + wave * TSZ;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = RS == 1 ? 16 * r + 4 * g + j : RS * (4 * g + j) + r;
+          Rw[row * NC + 16 * c + i] = acc[r][c][j];
+        }
+  }
+  __syncthreads();
+  const bool has = NCH % NT == 0 || tid < NCH;
+  f32x4v v[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int ch = has ? tid + j * NT : 0;
+    v[j] = *(const f32x4v *)&red[4 * ch];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v[j] += *(const f32x4v *)&red[w * TSZ + 4 * ch];
+  }
+  constexpr int IMODE = 1;
+  if (gridDim.y == 1) {
+    if (has) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], bias_r[j]);
+    }
+#ifdef BH_KTRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KT(4);
+#endif
+    return;
+  }
+  // ---- K chunks: slab [split][tile][TSZ] (write-through), ticket, last arriver combines
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)split * p.tiles_m * p.tiles_n + tile) * TSZ, TSZ * 4);
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]),
+                                             rw, 16 * (tid + j * NT), 0, AUX_SC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
+    if (last) __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+  // the K chunks' slabs summed in chunk order (as combine_tile), all loads of a slab in flight
+  if (!has) return;
+  const uint32_t tstep = TSZ * p.tiles_m * p.tiles_n * 4;
+  const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+  f32x4v sum[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  // four K chunks per round trip (missing ones read OOB zeros and are not added: same order)
+  const uint32_t S = gridDim.y;
+  for (uint32_t q = 0; q < S; q += 4) {
+    f32x4v x[4][CH];
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        x[i2][j] = __builtin_bit_cast(
+            f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                        rall, oob_unless(q + i2 < S, (q + i2) * tstep + (tile * TSZ + 4 * (uint32_t)(tid + j * NT)) * 4), 0,
+                        AUX_SC1));
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (q + i2 < S) sum[j] += x[i2][j];
+  }
+#pragma unroll
+  for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);
+}
+
 // NW waves split the block's K chunk; NG 16-deep k groups per register batch; DB: the next
 // batch's loads are issued before this batch's MFMAs (register double buffer)
 template <int R, int C, int NW, int NG, int DB, int BLD>
 __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
-  constexpr int NT = NW * 64, BMr = 16 * R, NC = 16 * C, KB = 16 * NG;
-  constexpr int TSZ = BMr * NC;         // floats of a block's output tile
-  constexpr int NCH = TSZ / 4, CH = (NCH + NT - 1) / NT;
-  static_assert(NCH % NT == 0 || NT % NCH == 0, "float4 chunks per thread");
-  __shared__ __attribute__((aligned(16))) float red[NW * TSZ + 4];
-  uint32_t *const flag = (uint32_t *)(red + NW * TSZ);
+  using G = gv_geom<R, C, NW>;
+  constexpr int BMr = G::BMr, NC = G::NC, KB = 16 * NG;
+  __shared__ __attribute__((aligned(16))) float red[NW * G::TSZ + 4];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   KT(0);
   const uint32_t tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m, split = blockIdx.y;
-  const uint32_t tile = blockIdx.x;
   const uint32_t m0 = tm * BMr;
   // this wave's share of the block's K chunk (p.ks: a multiple of NW * 16)
   const uint32_t kq = p.ks / NW;
@@ -104,15 +221,8 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
     }
   };
 
-  // bias of the rows this thread stores in the epilogue, fetched now (a dependent global
-  // load at the end of a small op costs a full memory round trip)
-  const bool has = NCH % NT == 0 || tid < NCH;
-  float bias_r[CH];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const uint32_t m = m0 + 4 * (uint32_t)(tid + j * NT) / NC;
-    bias_r[j] = (has && p.bias && m < p.M) ? p.bias[m] : 0.0f;
-  }
+  float bias_r[G::CH];
+  gv_bias<R, C, NW>(p, m0, tid, bias_r);
 
   f32x4t acc[R][C];
 #pragma unroll
@@ -166,84 +276,156 @@ __global__ __launch_bounds__(NW * 64) void gv_kernel(GemmArgs p) {
   }
 
   KT(2);
-  // ---- the NW waves' partial tiles -> LDS (row-major BMr x NC), summed in wave order.
-  // 16x16x4 C/D map: register j of lane l is row 4 * (l >> 4) + j, column l & 15.
-  {
-    float *const Rw = red + wave * TSZ;
+  gv_finish<R, C, NW, 1>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
+}
+
+// Loads of R consecutive floats (R = 1, 2, 4) at a per-lane offset + a scalar offset.
+template <int R>
+__device__ __forceinline__ typename fvec<R>::t ldv(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (R == 4)
+    return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  else if constexpr (R == 2)
+    return __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  else
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// gvp_kernel: the register-streaming structure of gv_kernel over the k-major packed bank
+// ([Kp][OC4], K order (ky, kx, ic): bh_conv_filts_pack, the xpose_filts role) for convs with
+// IC % 16 == 0, where every 16-deep k group lies inside one filter tap. gv_kernel's im2col
+// gather spends ~20 VALU per element on (ic, ky, kx) divisions and range checks; on a small op
+// that instruction stream IS the latency (a wave issues about one instruction per 4 clocks:
+// tools/lat_bench.hip). Here nothing per element is vector work:
+//  * A: MFMA step s of group gg takes packed row k = k16 + 4 s + g; one R-wide load per lane
+//    holds that row's entries for output channels m0 + R i .. m0 + R i + R - 1, so row rho of
+//    MFMA row tile r is block row R rho + r (gv_finish RS = R); the lane's channel offset is
+//    its VGPR address, the row offset (k16 + 4 s) * OC4 the instruction's scalar soffset;
+//  * B_IMTAP: the group's tap (ky, kx) and first channel ic0 are scalars; per column tile ONE
+//    per-lane offset (its input pixel at that tap, or a miss in the padding / past N) serves the
+//    group's four loads, whose channel offsets (ic0 + 4 s + g) * HW differ by scalar soffsets
+//    (the g part is folded into the lane's base); B_IM1X1S: the lane's pixel + the same
+//    scalar channel offsets;
+//  * a group past the wave's K range reads misses on both operands (one select per group).
+// The MFMA k map (step s, lane group g -> k16 + 4 s + g) is the same for A and B.
+template <int R, int C, int NW, int NG, int DB, int BLD>
+__global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
+  static_assert(BLD == B_IMTAP || BLD == B_IM1X1S, "gvp loaders: one-tap im2col or 1x1");
+  using G = gv_geom<R, C, NW>;
+  constexpr int BMr = G::BMr, NC = G::NC, KB = 16 * NG;
+  typedef typename fvec<R>::t av_t;
+  __shared__ __attribute__((aligned(16))) float red[NW * G::TSZ + 4];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  KT(0);
+  const uint32_t tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m, split = blockIdx.y;
+  const uint32_t m0 = tm * BMr;
+  // this wave's share of the block's K chunk (p.ks: a multiple of NW * 16)
+  const uint32_t kq = p.ks / NW;
+  const uint32_t kw0 = split * p.ks + wave * kq;
+  const uint32_t kw1 = min(p.K, kw0 + kq);
+  const int i = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
+  const uint32_t lda4 = p.lda * 4u, hw4 = p.HW * 4u;
+  // A: channels m0 + R i .. (one R-aligned group of the OC4-padded row, or all past it)
+  const uint32_t arow = oob_unless(m0 + R * i < p.lda, (m0 + R * i) * 4u + g * lda4);
+  // B: per column tile, the lane's input pixel for channel g at tap (0, 0)
+  uint32_t bcol[C];
+  int iy0[C], ix0[C];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Rw[(16 * r + 4 * g + j) * NC + 16 * c + i] = acc[r][c][j];
-  }
-  __syncthreads();
-  f32x4v v[CH];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int ch = has ? tid + j * NT : 0;
-    v[j] = *(const f32x4v *)&red[4 * ch];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) v[j] += *(const f32x4v *)&red[w * TSZ + 4 * ch];
-  }
-  constexpr int IMODE = 1;
-  if (gridDim.y == 1) {
-    if (has) {
-#pragma unroll
-      for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], bias_r[j]);
+  for (int c = 0; c < C; ++c) {
+    const uint32_t n = tn * NC + 16 * c + i;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    iy0[c] = 0;
+    ix0[c] = 0;
+    if constexpr (BLD == B_IM1X1S) {
+      bcol[c] = oob_unless(n < p.N, (img * p.ICHW + pix + g * p.HW) * 4u);
+    } else {
+      const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
+      iy0[c] = (int)(oy * p.sy) - (int)p.py;
+      ix0[c] = (int)(ox * p.sx) - (int)p.px;
+      bcol[c] = (uint32_t)((int)(img * p.ICHW + g * p.HW) + iy0[c] * (int)p.W + ix0[c]);
+      if (n >= p.N) iy0[c] = -(1 << 29);  // every tap misses
     }
-#ifdef BH_KTRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    KT(4);
-#endif
-    return;
   }
-  // ---- K chunks: slab [split][tile][TSZ] (write-through), ticket, last arriver combines
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)split * p.tiles_m * p.tiles_n + tile) * TSZ, TSZ * 4);
-  if (has) {
+
+  float bias_r[G::CH];
+  gv_bias<R, C, NW>(p, m0, tid, bias_r);
+
+  f32x4t acc[R][C];
 #pragma unroll
-    for (int j = 0; j < CH; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v[j]),
-                                             rw, 16 * (tid + j * NT), 0, AUX_SC1);
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[r][c] = f32x4t{0.0f, 0.0f, 0.0f, 0.0f};
+
+  av_t a0[NG][4], a1[DB ? NG : 1][4];
+  float b0[NG][4][C], b1[DB ? NG : 1][4][C];
+  auto load_batch = [&](uint32_t kb, av_t(&a)[NG][4], float(&b)[NG][4][C]) {
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg) {
+      const uint32_t k16 = kb + 16 * gg;
+      const bool live = k16 < kw1;  // wave-uniform
+      const uint32_t av = live ? arow : OOB;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[gg][s] = ldv<R>(rsa, av, (k16 + 4 * s) * lda4);
+      uint32_t bv[C];
+      uint32_t c0 = k16;
+      if constexpr (BLD == B_IM1X1S) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) bv[c] = live ? bcol[c] : OOB;
+      } else {
+        const uint32_t kyx = fdiv(k16, p.ic_m, p.ic_s);
+        const uint32_t ky = fdiv(kyx, p.kx_m, p.kx_s), kx = kyx - ky * p.KX;
+        c0 = k16 - kyx * p.IC;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const bool ok = live & ((uint32_t)(iy0[c] + (int)ky) < p.H) & ((uint32_t)(ix0[c] + (int)kx) < p.W);
+          bv[c] = oob_unless(ok, (uint32_t)((int)bcol[c] + (int)(ky * p.W + kx)) * 4u);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          b[gg][s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (c0 + 4 * s) * hw4, 0));
+    }
+  };
+  auto mma_batch = [&](const av_t(&a)[NG][4], const float(&b)[NG][4][C]) {
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(vget<R>(a[gg][s], r), b[gg][s][c], acc[r][c], 0, 0, 0);
+  };
+  uint32_t kb = kw0;
+  if constexpr (DB) {
+    if (kb < kw1) load_batch(kb, a0, b0);
+    while (kb < kw1) {
+      const uint32_t k1 = kb + KB;
+      if (k1 < kw1) load_batch(k1, a1, b1);
+      mma_batch(a0, b0);
+      if (kb == kw0) KT(1);
+      if (k1 >= kw1) break;
+      const uint32_t k2 = k1 + KB;
+      if (k2 < kw1) load_batch(k2, a0, b0);
+      mma_batch(a1, b1);
+      kb = k2;
+    }
+  } else {
+    for (; kb < kw1; kb += KB) {
+      load_batch(kb, a0, b0);
+      mma_batch(a0, b0);
+      if (kb == kw0) KT(1);
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(&p.cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
-    if (last) __hip_atomic_store(&p.cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
-  // the K chunks' slabs summed in chunk order (as combine_tile), all loads of a slab in flight
-  if (!has) return;
-  const uint32_t tstep = TSZ * p.tiles_m * p.tiles_n * 4;
-  const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
-  f32x4v sum[CH];
-#pragma unroll
-  for (int j = 0; j < CH; ++j) sum[j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  // four K chunks per round trip (missing ones read OOB zeros and are not added: same order)
-  const uint32_t S = gridDim.y;
-  for (uint32_t q = 0; q < S; q += 4) {
-    f32x4v x[4][CH];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < CH; ++j)
-        x[i][j] = __builtin_bit_cast(
-            f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                        rall, oob_unless(q + i < S, (q + i) * tstep + (tile * TSZ + 4 * (uint32_t)(tid + j * NT)) * 4), 0,
-                        AUX_SC1));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < CH; ++j)
-        if (q + i < S) sum[j] += x[i][j];
-  }
-#pragma unroll
-  for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);
+
+  KT(2);
+  gv_finish<R, C, NW, R>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
 }
 
 template <int R, int C, int NW, int NG, int DB>
@@ -253,6 +435,16 @@ cfg_t gv_cfg(const char *name) {
   c.k[A_MVEC][B_FC][0] = gv_kernel<R, C, NW, NG, DB, B_FC>;
   c.k[A_MVEC][B_IM1X1][0] = gv_kernel<R, C, NW, NG, DB, B_IM1X1>;
   c.k[A_MVEC][B_IM2COL][0] = gv_kernel<R, C, NW, NG, DB, B_IM2COL>;
+  return c;
+}
+
+// gvp configurations: the packed bank (packA), IC % 16 == 0 (launch_conv refuses others)
+template <int R, int C, int NW, int NG, int DB>
+cfg_t gvp_cfg(const char *name) {
+  cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 1};
+  c.gv = 1;
+  c.k[A_KVEC][B_IMTAP][0] = gvp_kernel<R, C, NW, NG, DB, B_IMTAP>;
+  c.k[A_KVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, NG, DB, B_IM1X1S>;
   return c;
 }
 
@@ -282,6 +474,21 @@ std::vector<cfg_t> gv_cfgs() {
       gv_cfg<1, 1, 16, 2, 1>("gv16x16w16"),
       gv_cfg<1, 2, 16, 2, 0>("gv16x32w16"),
       gv_cfg<2, 1, 16, 2, 0>("gv32x16w16"),
+      // over the packed bank with scalar-offset loaders (IC % 16 == 0)
+      gvp_cfg<1, 1, 4, 4, 1>("gvp16x16"),
+      gvp_cfg<1, 1, 8, 4, 1>("gvp16x16w8"),
+      gvp_cfg<1, 1, 16, 2, 1>("gvp16x16w16"),
+      gvp_cfg<1, 2, 8, 4, 1>("gvp16x32w8"),
+      gvp_cfg<1, 2, 16, 2, 0>("gvp16x32w16"),
+      gvp_cfg<2, 1, 8, 4, 1>("gvp32x16w8"),
+      gvp_cfg<2, 1, 16, 2, 0>("gvp32x16w16"),
+      gvp_cfg<2, 2, 4, 4, 1>("gvp32x32"),
+      gvp_cfg<2, 2, 8, 4, 1>("gvp32x32w8"),
+      gvp_cfg<2, 2, 16, 2, 0>("gvp32x32w16"),
+      gvp_cfg<4, 1, 4, 4, 1>("gvp64x16"),
+      gvp_cfg<4, 2, 8, 2, 1>("gvp64x32w8"),
+      gvp_cfg<2, 4, 8, 2, 1>("gvp32x64w8"),
+      gvp_cfg<4, 4, 8, 2, 0>("gvp64x64w8"),
   };
 }
 

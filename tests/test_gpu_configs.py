@@ -32,8 +32,10 @@ CONV_SHAPES = [
 ]
 
 
-# direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py
-@pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1)) if not n.startswith(("dc", "dm"))],
+# direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py;
+# gvp* only IC % 16 == 0: test_conv_gvp below
+@pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1))
+                                if not n.startswith(("dc", "dm", "gvp"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):
@@ -146,7 +148,7 @@ GV_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gv")])
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gv") and not n.startswith("gvp")])
 @pytest.mark.parametrize("splits", [0, 1, 5])
 def test_conv_gv(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
@@ -158,5 +160,49 @@ def test_conv_gv(dev, cn, splits):
             nm, rl2, _ = orc.normalized_errors(ref, out)
             assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
             np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed-order combine
+    finally:
+        dev.tune_set(1, -1, 0)
+
+
+# Register streaming over the packed bank (gvp*: IC % 16 == 0, one-tap / 1x1 scalar-offset
+# loaders): ragged M / N, K chunks ending inside a batch, taps in the padding, stride 2,
+# rows past OC4, several images per column tile
+GVP_SHAPES = [
+    ops.ConvShape(1, 160, 7, 7, 320, 3, 3, 1, 1, 1, 1),   # the small 3x3 ops (K 1440)
+    ops.ConvShape(2, 48, 14, 14, 70, 3, 3, 1, 1, 1, 1),   # ragged M (70), 392 columns
+    ops.ConvShape(5, 32, 7, 7, 100, 5, 5, 1, 1, 2, 2),    # 5x5 pad 2, 245 columns
+    ops.ConvShape(2, 64, 12, 11, 37, 5, 5, 2, 2, 2, 2),   # stride 2, OC 37 (OC4 40)
+    ops.ConvShape(5, 832, 7, 7, 48, 1, 1, 1, 1, 0, 0),    # 1x1, K 832
+    ops.ConvShape(3, 96, 6, 6, 70, 1, 1, 1, 1, 0, 0),     # 1x1, ragged
+    ops.ConvShape(1, 16, 9, 9, 20, 3, 3, 1, 1, 0, 0),     # K = 144: one group per tap
+    ops.ConvShape(4, 256, 6, 6, 130, 6, 6, 1, 1, 0, 0),   # fc-as-conv through the tap loader
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvp")])
+@pytest.mark.parametrize("splits", [0, 1, 3, 7])
+def test_conv_gvp(dev, cn, splits):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
+    try:
+        for s in GVP_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            ref = orc.conv_ref(i, f, b, s, 1)
+            nm, rl2, _ = orc.normalized_errors(ref, out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed-order combine
+            np.testing.assert_array_equal(run_conv(dev, s, packed=True), out)  # pre-packed bank
+        # host-made random operands (no symmetry a transposed row / k map could hide behind)
+        rng = np.random.default_rng(7)
+        for s in (GVP_SHAPES[1], GVP_SHAPES[3], GVP_SHAPES[5]):
+            hi = rng.standard_normal(s.B * s.IC * s.H * s.W).astype(np.float32)
+            hf = rng.standard_normal(s.OC * s.K).astype(np.float32)
+            hb = rng.standard_normal(s.OC).astype(np.float32)
+            out = run_conv(dev, s, host_inputs=(hi, hf, hb))
+            ref = orc.conv_ref(hi, hf, hb, s, 1)
+            nm, rl2, _ = orc.normalized_errors(ref, out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+        with pytest.raises(boda_hip.UnsupportedError):  # IC % 16 != 0
+            run_conv(dev, ops.ConvShape(1, 24, 7, 7, 32, 3, 3, 1, 1, 1, 1))
     finally:
         dev.tune_set(1, -1, 0)
