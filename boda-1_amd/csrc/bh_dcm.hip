@@ -133,23 +133,25 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
       sx[j] = ((c < (uint32_t)CI) & (x < p.W)) ? c * p.HW + x : 0xffffffffu;
     }
   }
-  // the strip offsets of the tile being issued (channel 0 of the stage; OOB where the element
-  // is padding or past the images), recomputed only when the issue side enters a new tile
-  uint32_t srel[LWB];
+  // the per-lane DMA offsets of the tile being issued (channel 0 of the stage; OOB where the
+  // element is padding, past the images or past the bank), recomputed only when the issue side
+  // enters a new tile; a stage adds its channel group's offset as the scalar soffset, so issuing
+  // a stage costs no vector work (every VALU op between f32 MFMAs is MFMA time lost)
+  uint32_t wvo[LWA], srel[LWB], bvo = OOB;
   uint32_t ls_tile = 0xffffffffu;
+  // a dead stage (past the block's iteration range) reads through zero-extent descriptors: all
+  // misses (zeros, no memory traffic), so every wave always has the same number in flight
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.b, 0u);
 
-  // Source offsets of this wave's LW DMA instructions for iteration `it` (tile it / ipt, channel
-  // group it % ipt); iterations past the block's range are all misses (OOB zeros, no memory
-  // traffic) so every wave always has the same number in flight and nothing branches
-  auto plan = [&](uint32_t it, uint32_t (&vo)[LW]) {
+  // scalar parts of iteration `it` (tile it / ipt, channel group it % ipt)
+  auto plan = [&](uint32_t it, uint32_t &sw, uint32_t &ss) -> bool {
     const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * CI;
-    uint32_t oc0, n0;
-    tile_of(t, oc0, n0);
-    const uint32_t dead = it < it1 ? 0u : OOB;
-    const uint32_t wlim = p.lda - min(oc0, p.lda), wb = (oc0 + ic0 * p.lda) * 4u;
-#pragma unroll
-    for (int j = 0; j < LWA; ++j) vo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
     if (t != ls_tile) {  // uniform
+      uint32_t oc0, n0;
+      tile_of(t, oc0, n0);
+      const uint32_t wlim = p.lda - min(oc0, p.lda);
+#pragma unroll
+      for (int j = 0; j < LWA; ++j) wvo[j] = oob_unless(wc4[j] < wlim, wrel[j] + oc0 * 4u);
       if constexpr (P1) {
 #pragma unroll
         for (int j = 0; j < LWB; ++j) {
@@ -159,33 +161,32 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
           srel[j] = oob_unless((sx[j] != 0xffffffffu) & (n < p.N), (img * p.ICHW + sx[j] + n - img * p.OHW) * 4u);
         }
       } else {
-      const uint32_t v0 = vrow0(n0);
+        const uint32_t v0 = vrow0(n0);
 #pragma unroll
-      for (int j = 0; j < LWB; ++j) {
-        const uint32_t vr = v0 + sr[j];
-        const uint32_t img = fdiv(vr, p.kyx_m, p.kyx_s);  // kyx fastdiv = H + 2py here
-        const uint32_t iy = vr - img * Hp - p.py;         // wraps (misses) in the top padding
-        const bool ok = (sx[j] != 0xffffffffu) & (iy < p.H) & (img < p.tiles_n);  // tiles_n = images
-        srel[j] = oob_unless(ok, (img * p.ICHW + iy * p.W + sx[j]) * 4u);
+        for (int j = 0; j < LWB; ++j) {
+          const uint32_t vr = v0 + sr[j];
+          const uint32_t img = fdiv(vr, p.kyx_m, p.kyx_s);  // kyx fastdiv = H + 2py here
+          const uint32_t iy = vr - img * Hp - p.py;         // wraps (misses) in the top padding
+          const bool ok = (sx[j] != 0xffffffffu) & (iy < p.H) & (img < p.tiles_n);  // tiles_n = images
+          srel[j] = oob_unless(ok, (img * p.ICHW + iy * p.W + sx[j]) * 4u);
+        }
       }
-      }
+      const uint32_t bo = (uint32_t)(64 * wave + lane);
+      bvo = oob_unless((bo < (uint32_t)OCT) & (oc0 + bo < p.M), (oc0 + bo) * 4u);
       ls_tile = t;
     }
-    // + the stage's channel offset: an OOB offset stays >= 2^31 (a miss)
-    const uint32_t chw4 = ic0 * p.HW * 4u;
-#pragma unroll
-    for (int j = 0; j < LWB; ++j) vo[LWA + j] = (srel[j] + chw4) | dead;
-    const uint32_t bo = (uint32_t)(64 * wave + lane);
-    vo[LW - 1] = oob_unless((bo < (uint32_t)OCT) & (oc0 + bo < p.M), (oc0 + bo) * 4u) | dead;
+    sw = ic0 * p.lda * 4u;
+    ss = ic0 * p.HW * 4u;
+    return it >= it1;
   };
-  auto issue_one = [&](int q, int slot, uint32_t vo) {
+  auto issue_one = [&](int q, int slot, uint32_t sw, uint32_t ss, bool dead) {
     float *const base = smem + slot * SLOT;
-    if (q < LWA) dma16(rsw, base + (wave * LWA + q) * 256, vo);
+    if (q < LWA) dma16s(dead ? rnull : rsw, base + (wave * LWA + q) * 256, wvo[q], sw);
     else if (q < LWA + LWB) {
-      if constexpr (V4) dma16(rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 256, vo);
-      else dma4(rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 64, vo);
+      if constexpr (V4) dma16s(dead ? rnull : rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 256, srel[q - LWA], ss);
+      else dma4s(dead ? rnull : rsi, base + WREG + GZ + (wave * LWB + q - LWA) * 64, srel[q - LWA], ss);
     }
-    else dma4(rsbias, base + WREG + GZ + SREG + 64 * wave, vo);
+    else dma4(dead ? rnull : rsbias, base + WREG + GZ + SREG + 64 * wave, bvo);
   };
 
   f32x16 acc[TM][TN];
@@ -194,8 +195,8 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
   // one stage = CI channels of one tile: STEPS steps of TM x TN MFMAs; iteration it_issue's DMAs
   // go out over the first IS steps; LDS fragments are read PF steps ahead
   auto compute = [&](int slot, int islot, uint32_t it_issue) {
-    uint32_t vo[LW];
-    plan(it_issue, vo);
+    uint32_t sw, ss;
+    const bool dead = plan(it_issue, sw, ss);
     // a lane's TM weight columns are adjacent (MFMA tile t, lane li: output channel TM*li + t of
     // the wave's group): one ds_read_b64 / b128 per step instead of TM ds_read_b32 (b32 reads
     // reach their rate only at ~4 waves per SIMD)
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
       if constexpr ((DBG & 1) == 0) {  // diagnostic build 1: no DMA after the prologue
 #pragma unroll
         for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
-          issue_one(q, islot, vo[q]);
+          issue_one(q, islot, sw, ss, dead);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -346,10 +347,10 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
   // ---- prologue: iterations it0 .. it0+D-2 in flight
 #pragma unroll
   for (int s = 0; s < D - 1; ++s) {
-    uint32_t vo[LW];
-    plan(it0 + (uint32_t)s, vo);
+    uint32_t sw, ss;
+    const bool dead = plan(it0 + (uint32_t)s, sw, ss);
 #pragma unroll
-    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+    for (int q = 0; q < LW; ++q) issue_one(q, s, sw, ss, dead);
   }
   int slot = 0;
   uint32_t it = it0;

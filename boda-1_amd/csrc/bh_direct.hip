@@ -78,7 +78,6 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   const uint32_t G = gridDim.x, b0 = blockIdx.x;
   const uint32_t ntile = p.total_it;  // tiles of the op
   const uint32_t my_tiles = b0 < ntile ? (ntile - b0 + G - 1) / G : 0;
-  const uint32_t nstage = my_tiles * p.IC;
   auto decode = [&](uint32_t t, uint32_t &oc0, uint32_t &img, uint32_t &p0) {
     const uint32_t rest = fdiv(t, p.ipt_m, p.ipt_s);  // ipt = OC tiles
     oc0 = (t - rest * p.ipt) * OCT;
@@ -109,30 +108,33 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     srel[j] = (r * p.W + (uint32_t)x) * 4u;
   }
 
-  // Source offsets of this wave's LW DMA instructions for block stage g (tile g / IC, input
-  // channel g % IC); stages past the block's last tile are all misses (OOB zeros, no memory
-  // traffic) so every wave always has the same number in flight and nothing branches
-  auto plan = [&](uint32_t g, uint32_t (&vo)[LW]) {
-    const uint32_t i = fdiv(g, p.ic_m, p.ic_s), ic = g - i * p.IC;
+  // DMA sources of block stage g (tile g / IC, input channel g % IC): the per-lane part depends
+  // on the tile only and is planned once per tile (tvo, VGPRs); the channel's part is a scalar
+  // soffset (ic * HW for the strip, ic * OC4 for the bank rows), so issuing a stage costs no
+  // vector work -- every VALU op between f32 MFMAs is MFMA time lost (one wave per SIMD).
+  // Stages past the block's last tile belong to a dead tile: all misses (OOB zeros, no memory
+  // traffic), so every wave always has the same number of DMAs in flight and nothing branches.
+  uint32_t tvo[LW];
+  auto plan_tile = [&](uint32_t i) {
     uint32_t oc0, img, p0;
     decode(b0 + i * G, oc0, img, p0);
-    const uint32_t dead = g < nstage ? 0u : OOB;
-    const uint32_t wlim = p.lda - min(oc0, p.lda), wb = (oc0 + ic * p.lda) * 4u;
+    const uint32_t dead = i < my_tiles ? 0u : OOB;
+    const uint32_t wlim = p.lda - min(oc0, p.lda), wb = oc0 * 4u;
 #pragma unroll
-    for (int j = 0; j < LWA; ++j) vo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
+    for (int j = 0; j < LWA; ++j) tvo[j] = oob_unless(wc4[j] < wlim, wrel[j] + wb) | dead;
     const int ya = (int)(fdiv(p0, p.ow_m, p.ow_s) * S) - (int)p.py;  // input row of strip row 0
     const uint32_t rlo = (uint32_t)max(0, -ya), rhi = (uint32_t)max(0, (int)p.H - ya);
-    const uint32_t sb = (img * p.ICHW + ic * p.HW) * 4u + (uint32_t)(ya * (int)p.W) * 4u;
+    const uint32_t sb = img * p.ICHW * 4u + (uint32_t)(ya * (int)p.W) * 4u;
 #pragma unroll
     for (int j = 0; j < LWB; ++j)
-      vo[LWA + j] = oob_unless((srow[j] >= rlo) & (srow[j] < rhi), srel[j] + sb) | dead;
-    vo[LW - 1] = oob_unless((uint32_t)(64 * wave + lane) < (uint32_t)OCT, (oc0 + 64 * wave + lane) * 4u) | dead;
+      tvo[LWA + j] = oob_unless((srow[j] >= rlo) & (srow[j] < rhi), srel[j] + sb) | dead;
+    tvo[LW - 1] = oob_unless((uint32_t)(64 * wave + lane) < (uint32_t)OCT, (oc0 + 64 * wave + lane) * 4u) | dead;
   };
-  auto issue_one = [&](int q, int slot, uint32_t vo) {
+  auto issue_one = [&](int q, int slot, uint32_t ic) {
     float *const base = smem + slot * SLOT;
-    if (q < LWA) dma16(rsw, base + (wave * LWA + q) * 256, vo);
-    else if (q < LWA + LWB) dma4(rsi, base + WREG + (wave * LWB + q - LWA) * 64, vo);
-    else dma4(rsbias, base + WREG + SREG + 64 * wave, vo);
+    if (q < LWA) dma16s(rsw, base + (wave * LWA + q) * 256, tvo[q], ic * p.lda * 4u);
+    else if (q < LWA + LWB) dma4s(rsi, base + WREG + (wave * LWB + q - LWA) * 64, tvo[q], ic * p.HW * 4u);
+    else dma4(rsbias, base + WREG + SREG + 64 * wave, tvo[q]);
   };
 
   f32x16 acc[TM][TN];
@@ -156,21 +158,35 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   // DMAs are issued over the first IS steps, the previous tile's deferred stores (if any) over
   // the first ISS; LDS fragments are read PF steps ahead
   auto compute = [&](int slot, int islot, uint32_t g_issue, bool dstores) {
-    uint32_t vo[LW];
-    plan(g_issue, vo);
+    const uint32_t i_issue = fdiv(g_issue, p.ic_m, p.ic_s), ic_issue = g_issue - i_issue * p.IC;
+    if (ic_issue == 0) plan_tile(i_issue);  // wave-uniform
     const float *const Ab = smem + slot * SLOT + kh * KK2 * OCT + li;
     const char *const Sb = (const char *)(smem + slot * SLOT + WREG);
-    // opaque per stage: otherwise hipcc hoists every step's (lane half -> tap offset) select out
-    // of the stage loop and keeps KK2 of them live
+    // Lane half 1 reads tap KK2 + s where half 0 reads tap s: its strip offset is larger by
+    // dk(s) = koff(KK2 + s) - koff(s), which takes only two values over the real taps (DLO while
+    // the column shift KK2 % KX does not wrap, DHI when it does) and a third at the padding
+    // tap (KK odd: the last step; zero weights, so any in-strip offset -- tap 0). Three per-lane
+    // bases per stage, then every step's B fragment is one ds_read at base + a compile-time
+    // immediate: no per-step select or add (each VALU op between f32 MFMAs is MFMA time lost).
+    constexpr int CSH = KK2 % KX, RSH = KK2 / KX;
+    constexpr int DLO = RSH * WPM + CSH, DHI = (RSH + 1) * WPM + CSH - KX;
+    constexpr int DPAD = -dc_koff<KX, WPM>(KK2 - 1, KK);
+    // opaque per stage: keeps the bases' lane-half selects from being rematerialized per step
     asm volatile("" : "+v"(hsel));
+    const char *bs[3][TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      bs[0][tn] = Sb + poff[tn] + (hsel & (uint32_t)(DLO * 4));
+      bs[1][tn] = Sb + poff[tn] + (hsel & (uint32_t)(DHI * 4));
+      bs[2][tn] = Sb + poff[tn] + (int)(hsel & (uint32_t)(DPAD * 4));
+    }
     auto frag = [&](int s, float (&a)[TM], float (&b)[TN]) {
 #pragma unroll
       for (int t = 0; t < TM; ++t) a[t] = Ab[s * OCT + 32 * t];
-      const uint32_t k0 = (uint32_t)dc_koff<KX, WPM>(s, KK) * 4u;
-      const uint32_t dk = (uint32_t)(dc_koff<KX, WPM>(KK2 + s, KK) - dc_koff<KX, WPM>(s, KK)) * 4u;
-      const uint32_t ko = k0 + (hsel & dk);
+      const int k0 = dc_koff<KX, WPM>(s, KK) * 4;
+      const int kind = KK2 + s >= KK ? 2 : (s % KX < KX - CSH ? 0 : 1);
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(Sb + poff[tn] + ko);
+      for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(bs[kind][tn] + k0);
     };
     float a[PF + 1][TM], b[PF + 1][TN];
 #pragma unroll
@@ -189,7 +205,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
       // most of a stage to land before the wait that retires it (the very next stage at D = 2)
 #pragma unroll
       for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q)
-        issue_one(q, islot, vo[q]);
+        issue_one(q, islot, ic_issue);
       if (dstores) {
 #pragma unroll
         for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
@@ -201,10 +217,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   // ---- prologue: stages 0 .. D-2 in flight
 #pragma unroll
   for (int s = 0; s < D - 1; ++s) {
-    uint32_t vo[LW];
-    plan((uint32_t)s, vo);
+    const uint32_t i_s = fdiv((uint32_t)s, p.ic_m, p.ic_s), ic_s = (uint32_t)s - i_s * p.IC;
+    if (ic_s == 0) plan_tile(i_s);
 #pragma unroll
-    for (int q = 0; q < LW; ++q) issue_one(q, s, vo[q]);
+    for (int q = 0; q < LW; ++q) issue_one(q, s, ic_s);
   }
   const bool vec = p.cvec != 0 && !p.res;  // float4 pieces, deferred (else stored at once)
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);

@@ -127,13 +127,16 @@ __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
 // of tile (tile_m, tile_n): dense C rows, or NCHW scatter for conv (IMODE). p.cvec: rows
 // take aligned float4 stores (dense: ldc % 4 == 0; conv: OH*OW % 4 == 0).
 // finish_store_b: the same with the chunk's bias value already in hand (prefetched)
-template <int IMODE>
+// (TBN > 0: the tile width p.tbn as a compile-time constant -- a run-time udiv is ~25 VALU on a
+// small op's critical path)
+template <int IMODE, int TBN = 0>
 __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_m, uint32_t tile_n, uint32_t c,
                                                f32x4v sum, float b) {
-  const uint32_t e0 = 4 * c, row = e0 / p.tbn, col0 = e0 - row * p.tbn;
+  const uint32_t tbn = TBN > 0 ? (uint32_t)TBN : p.tbn;
+  const uint32_t e0 = 4 * c, row = e0 / tbn, col0 = e0 - row * tbn;
   const uint32_t m = tile_m * p.tbm + row;
   if (m >= p.M) return;
-  const uint32_t n0 = tile_n * p.tbn + col0;
+  const uint32_t n0 = tile_n * tbn + col0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) sum[t] += b;
   if (p.cvec && n0 + 4 <= p.N) {
@@ -298,6 +301,9 @@ __device__ __forceinline__ void dma4s(__amdgpu_buffer_rsrc_t r, const float *lds
 }
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, 0);
 }
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const float *lds, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, 0, 0, 0);

@@ -92,7 +92,7 @@ __device__ __forceinline__ void gv_finish(const GemmArgs &p, f32x4t (&acc)[R][C]
   if (gridDim.y == 1) {
     if (has) {
 #pragma unroll
-      for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], bias_r[j]);
+      for (int j = 0; j < CH; ++j) finish_store_b<IMODE, NC>(p, tm, tn, (uint32_t)(tid + j * NT), v[j], bias_r[j]);
     }
 #ifdef BH_KTRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -145,7 +145,7 @@ __device__ __forceinline__ void gv_finish(const GemmArgs &p, f32x4t (&acc)[R][C]
         if (q + i2 < S) sum[j] += x[i2][j];
   }
 #pragma unroll
-  for (int j = 0; j < CH; ++j) finish_store_b<IMODE>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);
+  for (int j = 0; j < CH; ++j) finish_store_b<IMODE, NC>(p, tm, tn, (uint32_t)(tid + j * NT), sum[j], bias_r[j]);
 }
 
 // NW waves split the block's K chunk; NG 16-deep k groups per register batch; DB: the next
