@@ -247,7 +247,11 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
 
   const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
-  const bool vec = p.cvec != 0 && !p.res;  // float4 pixel quads (OHW % 4 == 0: a quad is in one image)
+  // float4 pixel quads, at any dword alignment (the output row of a channel starts at m * OHW);
+  // a quad running past its image's last pixel (OHW % 4 != 0) goes element by element. Element
+  // stores for every quad scatter each wave instruction over 32 rows: 4x the store instructions
+  // and line writes of the quads (the 13x13 / 27x27 ops)
+  const bool vec = !p.res;
 
   // bias, residual, ReLU and store of a tile's values: v[q], q = (t, tn, gq) holds output channel
   // oc0 + wo*32*TM + TM*li + t, pixels n0 + wp*32*TN + 32 tn + 8 gq + 4 kh + e (e = 0..3)
@@ -262,16 +266,16 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
         for (int gq = 0; gq < 4; ++gq) {
           f32x4v x = v[(t * TN + tn) * 4 + gq];
           const uint32_t nq = n0 + (uint32_t)(wp * 32 * TN + 32 * tn + 8 * gq + 4 * kh);
-          if (vec) {
-            const uint32_t img = fdiv(nq, p.ohw_m, p.ohw_s);
-            const uint32_t o = oob_unless((m < p.M) & (nq < p.N), (img * p.OCOHW + m * p.OHW + nq - img * p.OHW) * 4u);
+          const uint32_t img = fdiv(nq, p.ohw_m, p.ohw_s), pix = nq - img * p.OHW;
+          if (vec && pix + 4 <= p.OHW) {
+            const uint32_t o = oob_unless((m < p.M) & (nq < p.N), (img * p.OCOHW + m * p.OHW + pix) * 4u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               x[e] += bb;
               x[e] = (p.relu && x[e] < 0.0f) ? 0.0f : x[e];
             }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, x),
-                                                   rso, o, 0, 0);
+                                                   rso, o, 0, AUX_OUT);
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
               float y = x[e] + bb;
               if (p.res) y += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
               y = (p.relu && y < 0.0f) ? 0.0f : y;
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, y), rso, o, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, y), rso, o, 0, AUX_OUT);
             }
           }
         }

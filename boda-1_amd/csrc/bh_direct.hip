@@ -28,13 +28,6 @@
 namespace bhk {
 namespace {
 
-// blocks b, b+8, b+16, ... share an XCD under round-robin placement: give them consecutive
-// pixel tiles (their input strips overlap by the halo rows) -- bijective for any count
-__device__ __forceinline__ uint32_t dc_remap(uint32_t bid, uint32_t n) {
-  const uint32_t xcd = bid & 7, q = n >> 3, r = n & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
 template <int KX, int WPM>
 constexpr int dc_koff(int tap, int KK) {
   return tap < KK ? (tap / KX) * WPM + tap % KX : 0;  // padding taps (zero weights): any in-strip offset
@@ -147,11 +140,21 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   uint32_t dbase[TM], dpx = 0, dhw = 0;  // piece (t, tn, gq): byte offset dbase[t] + 4 (32 tn + 8 gq), pixel
                                          // dpx + 32 tn + 8 gq (dropped at >= dhw: past the image)
   const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  // (any dword alignment: OHW % 4 != 0 puts a channel's row at m * OHW; a piece running past the
+  // image's last pixel goes element by element)
   auto store_one = [&](int q) {
     const int t = q / (TN * 4), tn = (q / 4) % TN, gq = q % 4;
-    const uint32_t off = oob_unless(dpx + (uint32_t)(32 * tn + 8 * gq) < dhw, dbase[t] + (uint32_t)(32 * tn + 8 * gq) * 4u);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
-                                           rso, off, 0, 0);
+    const uint32_t px = dpx + (uint32_t)(32 * tn + 8 * gq);
+    const uint32_t off = dbase[t] + (uint32_t)(32 * tn + 8 * gq) * 4u;
+    if (px + 4 <= dhw) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
+                                             rso, off, 0, AUX_OUT);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dval[q][e]), rso,
+                                              oob_unless(px + (uint32_t)e < dhw, off + 4u * (uint32_t)e), 0, AUX_OUT);
+    }
   };
 
   // one stage = one input channel of one tile: KK2 steps of TM x TN MFMAs; stage g_issue's
@@ -222,7 +225,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #pragma unroll
     for (int q = 0; q < LW; ++q) issue_one(q, s, ic_s);
   }
-  const bool vec = p.cvec != 0 && !p.res;  // float4 pieces, deferred (else stored at once)
+  const bool vec = !p.res;  // float4 pieces, deferred (else stored at once)
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
   bool pending = false;  // deferred stores of the previous tile not yet issued
   int slot = 0;
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
             float x = acc[t][tn][r] + bb;
             if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
             x = (p.relu && x < 0.0f) ? 0.0f : x;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, AUX_OUT);
           }
       }
     }

@@ -1150,8 +1150,9 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   p.a_bytes = (uint32_t)w_bytes;
   p.b_bytes = (uint32_t)in_bytes;
   p.relu = relu;
-  p.cvec = (OH * OW) % 4 == 0 && ((uintptr_t)out % 16 == 0) &&
-           ((uintptr_t)res % 16 == 0);  // output (and residual) rows take float4 accesses
+  // output (and residual) rows take float4 accesses (dword-aligned tensors: any OH*OW; a quad
+  // of columns running past its image is stored element by element)
+  p.cvec = ((uintptr_t)out % 4 == 0) && ((uintptr_t)res % 4 == 0);
   p.H = H; p.W = W; p.KX = KX; p.KYX = KY * KX;
   p.sy = sy; p.sx = sx; p.py = py; p.px = px;
   p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = out_ctot * OH * OW;

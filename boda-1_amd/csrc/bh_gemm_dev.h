@@ -139,11 +139,14 @@ __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_
   const uint32_t n0 = tile_n * tbn + col0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) sum[t] += b;
-  if (p.cvec && n0 + 4 <= p.N) {
+  // conv: four columns in one image are four adjacent floats of the output row, at any dword
+  // alignment (OHW % 4 != 0 puts channel m's row at m * OHW; the hardware takes unaligned
+  // dword-multiple accesses); element stores scatter a wave instruction over 4x the rows
+  const uint32_t img0 = IMODE ? fdiv(n0, p.ohw_m, p.ohw_s) : 0u, pix0 = n0 - img0 * p.OHW;
+  if (IMODE ? (p.cvec && n0 + 4 <= p.N && pix0 + 4 <= p.OHW) : (p.cvec && n0 + 4 <= p.N)) {
     size_t o;
     if constexpr (IMODE) {
-      const uint32_t img = fdiv(n0, p.ohw_m, p.ohw_s);
-      o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n0 - img * p.OHW);
+      o = (size_t)img0 * p.OCOHW + (size_t)m * p.OHW + pix0;
       if (p.res) sum += *(const f32x4v *)&p.res[o];
     } else {
       o = (size_t)m * p.ldc + n0;
@@ -178,6 +181,13 @@ __device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m,
 }
 
 constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
+// Final output stores: write-through. Dirty L2 lines left at the end of a kernel are written back
+// at the kernel boundary, before the next launch in the stream starts (MI355X_MICROARCH.md,
+// boundary row: + bytes / ~6 TB/s); written through during the kernel they overlap the compute.
+#ifndef BH_AUX_OUT
+#define BH_AUX_OUT 0
+#endif
+constexpr int AUX_OUT = BH_AUX_OUT;
 
 // Split-K combine of one float4 chunk c for the reduce kernel (after a kernel boundary,
 // so plain loads): the S slabs summed in fixed order, four in flight.
