@@ -307,7 +307,11 @@ __device__ __forceinline__ typename fvec<R>::t ldv(__amdgpu_buffer_rsrc_t r, uin
 //    scalar channel offsets;
 //  * a group past the wave's K range reads misses on both operands (one select per group).
 // The MFMA k map (step s, lane group g -> k16 + 4 s + g) is the same for A and B.
-template <int R, int C, int NW, int NG, int DB, int BLD>
+// PD > 0: instead of batches, a ring of PD + 1 single-group register buffers -- the loads of
+// group g + PD are issued before group g's MFMAs, so PD groups of loads are always in flight
+// (the batch form with DB = 0 exposes a whole memory round trip per batch; DB = 1 doubles its
+// registers)
+template <int R, int C, int NW, int NG, int DB, int BLD, int PD = 0>
 __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   static_assert(BLD == B_IMTAP || BLD == B_IM1X1S, "gvp loaders: one-tap im2col or 1x1");
   using G = gv_geom<R, C, NW>;
@@ -359,48 +363,79 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
 #pragma unroll
     for (int c = 0; c < C; ++c) acc[r][c] = f32x4t{0.0f, 0.0f, 0.0f, 0.0f};
 
+  // loads of the 16-deep k group at k16 into one group buffer (misses past the wave's range)
+  auto load_grp = [&](uint32_t k16, av_t(&a)[4], float(&b)[4][C]) {
+    const bool live = k16 < kw1;  // wave-uniform
+    const uint32_t av = live ? arow : OOB;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a[s] = ldv<R>(rsa, av, (k16 + 4 * s) * lda4);
+    uint32_t bv[C];
+    uint32_t c0 = k16;
+    if constexpr (BLD == B_IM1X1S) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) bv[c] = live ? bcol[c] : OOB;
+    } else {
+      const uint32_t kyx = fdiv(k16, p.ic_m, p.ic_s);
+      const uint32_t ky = fdiv(kyx, p.kx_m, p.kx_s), kx = kyx - ky * p.KX;
+      c0 = k16 - kyx * p.IC;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const bool ok = live & ((uint32_t)(iy0[c] + (int)ky) < p.H) & ((uint32_t)(ix0[c] + (int)kx) < p.W);
+        bv[c] = oob_unless(ok, (uint32_t)((int)bcol[c] + (int)(ky * p.W + kx)) * 4u);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        b[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (c0 + 4 * s) * hw4, 0));
+  };
+  auto mma_grp = [&](const av_t(&a)[4], const float(&b)[4][C]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(vget<R>(a[s], r), b[s][c], acc[r][c], 0, 0, 0);
+  };
+  if constexpr (PD > 0) {
+    constexpr int RING = PD + 1;
+    av_t ra[RING][4];
+    float rb[RING][4][C];
+#pragma unroll
+    for (int r = 0; r < PD; ++r) load_grp(kw0 + 16u * r, ra[r], rb[r]);
+    // whole trips of RING groups (no exits inside: the loop head sees the same PD groups in
+    // flight from the prologue and from the back edge, so the waits stay counted), then a tail
+    auto step = [&](int r, uint32_t kc) {
+      // pinned order: the prefetch loads, then this group's MFMAs (else hipcc interleaves them
+      // and waits on the prefetch)
+      __builtin_amdgcn_sched_barrier(0);
+      load_grp(kc + 16u * PD, ra[(r + PD) % RING], rb[(r + PD) % RING]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_grp(ra[r % RING], rb[r % RING]);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    const uint32_t ngrp = kw1 > kw0 ? (kw1 - kw0 + 15) / 16 : 0;
+    uint32_t k = kw0, g = 0;
+    for (; g + RING <= ngrp; g += RING, k += 16u * RING) {
+#pragma unroll
+      for (int r = 0; r < RING; ++r) step(r, k + 16u * r);
+      if (g == 0) KT(1);
+    }
+#pragma unroll
+    for (int r = 0; r < RING - 1; ++r)
+      if (g + r < ngrp) step(r, k + 16u * r);
+  } else {
   av_t a0[NG][4], a1[DB ? NG : 1][4];
   float b0[NG][4][C], b1[DB ? NG : 1][4][C];
   auto load_batch = [&](uint32_t kb, av_t(&a)[NG][4], float(&b)[NG][4][C]) {
 #pragma unroll
-    for (int gg = 0; gg < NG; ++gg) {
-      const uint32_t k16 = kb + 16 * gg;
-      const bool live = k16 < kw1;  // wave-uniform
-      const uint32_t av = live ? arow : OOB;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) a[gg][s] = ldv<R>(rsa, av, (k16 + 4 * s) * lda4);
-      uint32_t bv[C];
-      uint32_t c0 = k16;
-      if constexpr (BLD == B_IM1X1S) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) bv[c] = live ? bcol[c] : OOB;
-      } else {
-        const uint32_t kyx = fdiv(k16, p.ic_m, p.ic_s);
-        const uint32_t ky = fdiv(kyx, p.kx_m, p.kx_s), kx = kyx - ky * p.KX;
-        c0 = k16 - kyx * p.IC;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const bool ok = live & ((uint32_t)(iy0[c] + (int)ky) < p.H) & ((uint32_t)(ix0[c] + (int)kx) < p.W);
-          bv[c] = oob_unless(ok, (uint32_t)((int)bcol[c] + (int)(ky * p.W + kx)) * 4u);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-          b[gg][s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (c0 + 4 * s) * hw4, 0));
-    }
+    for (int gg = 0; gg < NG; ++gg) load_grp(kb + 16 * gg, a[gg], b[gg]);
   };
   auto mma_batch = [&](const av_t(&a)[NG][4], const float(&b)[NG][4][C]) {
 #pragma unroll
-    for (int gg = 0; gg < NG; ++gg)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < C; ++c)
-            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(vget<R>(a[gg][s], r), b[gg][s][c], acc[r][c], 0, 0, 0);
+    for (int gg = 0; gg < NG; ++gg) mma_grp(a[gg], b[gg]);
   };
   uint32_t kb = kw0;
   if constexpr (DB) {
@@ -424,6 +459,8 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
     }
   }
 
+  }
+
   KT(2);
   gv_finish<R, C, NW, R>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
 }
@@ -439,12 +476,12 @@ cfg_t gv_cfg(const char *name) {
 }
 
 // gvp configurations: the packed bank (packA), IC % 16 == 0 (launch_conv refuses others)
-template <int R, int C, int NW, int NG, int DB>
+template <int R, int C, int NW, int NG, int DB, int PD = 0>
 cfg_t gvp_cfg(const char *name) {
   cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 1};
   c.gv = 1;
-  c.k[A_KVEC][B_IMTAP][0] = gvp_kernel<R, C, NW, NG, DB, B_IMTAP>;
-  c.k[A_KVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, NG, DB, B_IM1X1S>;
+  c.k[A_KVEC][B_IMTAP][0] = gvp_kernel<R, C, NW, NG, DB, B_IMTAP, PD>;
+  c.k[A_KVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, NG, DB, B_IM1X1S, PD>;
   return c;
 }
 
@@ -489,6 +526,16 @@ std::vector<cfg_t> gv_cfgs() {
       gvp_cfg<4, 2, 8, 2, 1>("gvp64x32w8"),
       gvp_cfg<2, 4, 8, 2, 1>("gvp32x64w8"),
       gvp_cfg<4, 4, 8, 2, 0>("gvp64x64w8"),
+      // the same with a ring of single-group buffers, PD groups of loads in flight
+      gvp_cfg<4, 4, 8, 1, 0, 2>("gvs64x64w8"),
+      gvp_cfg<4, 4, 4, 1, 0, 3>("gvs64x64"),
+      gvp_cfg<4, 2, 8, 1, 0, 2>("gvs64x32w8"),
+      gvp_cfg<2, 4, 8, 1, 0, 2>("gvs32x64w8"),
+      gvp_cfg<2, 2, 8, 1, 0, 3>("gvs32x32w8"),
+      gvp_cfg<2, 2, 16, 1, 0, 2>("gvs32x32w16"),
+      gvp_cfg<2, 1, 16, 1, 0, 2>("gvs32x16w16"),
+      gvp_cfg<1, 1, 16, 1, 0, 2>("gvs16x16w16"),
+      gvp_cfg<1, 1, 8, 1, 0, 3>("gvs16x16w8"),
   };
 }
 

@@ -35,7 +35,7 @@ CONV_SHAPES = [
 # direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py;
 # gvp* only IC % 16 == 0: test_conv_gvp below
 @pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1))
-                                if not n.startswith(("dc", "dm", "gvp"))],
+                                if not n.startswith(("dc", "dm", "gvp", "gvs"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):
@@ -148,7 +148,8 @@ GV_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gv") and not n.startswith("gvp")])
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1)
+                                if n.startswith("gv") and not n.startswith(("gvp", "gvs"))])
 @pytest.mark.parametrize("splits", [0, 1, 5])
 def test_conv_gv(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
@@ -164,8 +165,8 @@ def test_conv_gv(dev, cn, splits):
         dev.tune_set(1, -1, 0)
 
 
-# Register streaming over the packed bank (gvp*: IC % 16 == 0, one-tap / 1x1 scalar-offset
-# loaders): ragged M / N, K chunks ending inside a batch, taps in the padding, stride 2,
+# Register streaming over the packed bank (gvp* / gvs*: IC % 16 == 0, one-tap / 1x1 scalar-offset
+# loaders; gvs: the ring of single-group buffers, whole trips + tail): ragged M / N, K chunks ending inside a batch, taps in the padding, stride 2,
 # rows past OC4, several images per column tile
 GVP_SHAPES = [
     ops.ConvShape(1, 160, 7, 7, 320, 3, 3, 1, 1, 1, 1),   # the small 3x3 ops (K 1440)
@@ -176,10 +177,11 @@ GVP_SHAPES = [
     ops.ConvShape(3, 96, 6, 6, 70, 1, 1, 1, 1, 0, 0),     # 1x1, ragged
     ops.ConvShape(1, 16, 9, 9, 20, 3, 3, 1, 1, 0, 0),     # K = 144: one group per tap
     ops.ConvShape(4, 256, 6, 6, 130, 6, 6, 1, 1, 0, 0),   # fc-as-conv through the tap loader
+    ops.ConvShape(1, 512, 7, 7, 64, 3, 3, 1, 1, 1, 1),    # K 4608: many whole ring trips per wave
 ]
 
 
-@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvp")])
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("gvp", "gvs"))])
 @pytest.mark.parametrize("splits", [0, 1, 3, 7])
 def test_conv_gvp(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
