@@ -536,6 +536,13 @@ std::vector<cfg_t> gv_cfgs() {
       gvp_cfg<2, 1, 16, 1, 0, 2>("gvs32x16w16"),
       gvp_cfg<1, 1, 16, 1, 0, 2>("gvs16x16w16"),
       gvp_cfg<1, 1, 8, 1, 0, 3>("gvs16x16w8"),
+      gvp_cfg<4, 2, 16, 1, 0, 2>("gvs64x32w16"),
+      gvp_cfg<2, 4, 16, 1, 0, 2>("gvs32x64w16"),
+      gvp_cfg<4, 2, 8, 1, 0, 3>("gvs64x32w8p3"),
+      gvp_cfg<4, 4, 8, 1, 0, 1>("gvs64x64w8p1"),
+      gvp_cfg<4, 1, 16, 1, 0, 2>("gvs64x16w16"),
+      gvp_cfg<1, 2, 16, 1, 0, 2>("gvs16x32w16"),
+      gvp_cfg<4, 2, 4, 1, 0, 3>("gvs64x32"),
   };
 }
 

@@ -44,7 +44,8 @@ def bk_of(name):
     if name.startswith(("dc", "dm")):
         return 1 << 30
     if name.startswith("gv"):
-        return 16 * (int(name.split("w")[1]) if "w" in name else 4)
+        m = re.search(r"w(\d+)", name)
+        return 16 * (int(m.group(1)) if m else 4)
     return int(re.match(r"\d+", name.split("x")[2]).group(0))
 
 
