@@ -33,7 +33,11 @@ constexpr int dc_koff(int tap, int KK) {
   return tap < KK ? (tap / KX) * WPM + tap % KX : 0;  // padding taps (zero weights): any in-strip offset
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D>
+// V4: input rows of W % 4 == 0 go into the strip as 16-B pieces (a quarter of the DMA
+// instructions: the strip's dword DMAs were 0.34 issues per MFMA at 11x11 s4); column c of the
+// strip then holds input x = c - PXA with PXA = 4 (0 without horizontal padding), so pieces start
+// on 16-B input boundaries
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0>
 __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int NW = 4;
   constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
@@ -42,8 +46,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int LWA = (WPC + NW * 64 - 1) / (NW * 64);    // weight DMA instructions per wave
   constexpr int WREG = LWA * NW * 256;                    // floats
   constexpr int SF = RIN * WPM;
-  constexpr int LWB = (SF + NW * 64 - 1) / (NW * 64);     // strip DMA instructions per wave
-  constexpr int SREG = LWB * NW * 64;
+  constexpr int PW = V4 ? 4 : 1;                          // floats per strip DMA lane
+  static_assert(WPM % PW == 0, "16-B strip rows");
+  constexpr int LWB = (SF / PW + NW * 64 - 1) / (NW * 64);  // strip DMA instructions per wave
+  constexpr int SREG = LWB * NW * 64 * PW;
   constexpr int BREG = NW * 64;                           // the stage tile's biases, one DMA per wave
   constexpr int SLOT = WREG + SREG + BREG;
   constexpr int LW = LWA + LWB + 1;
@@ -92,11 +98,13 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     wc4[j] = tap < (uint32_t)KK ? 4 * (e % (OCT / 4)) : 0xffffu;
     wrel[j] = (tap * p.IC * p.lda + 4 * (e % (OCT / 4))) * 4u;
   }
+  const uint32_t pxa = V4 ? (p.px ? 4u : 0u) : p.px;  // strip column of input x = 0
 #pragma unroll
   for (int j = 0; j < LWB; ++j) {
-    const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane);
+    const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane) * PW;  // first strip element of the lane
     const uint32_t r = e / WPM, c = e - (e / WPM) * WPM;
-    const int x = (int)c - (int)p.px;
+    const int x = (int)c - (int)pxa;
+    // V4: a piece is inside the row or outside it as a whole (W % 4 == 0, pxa % 4 == 0)
     srow[j] = ((r < (uint32_t)RIN) & ((uint32_t)x < p.W)) ? r : 0xffffu;
     srel[j] = (r * p.W + (uint32_t)x) * 4u;
   }
@@ -126,7 +134,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   auto issue_one = [&](int q, int slot, uint32_t ic) {
     float *const base = smem + slot * SLOT;
     if (q < LWA) dma16s(rsw, base + (wave * LWA + q) * 256, tvo[q], ic * p.lda * 4u);
-    else if (q < LWA + LWB) dma4s(rsi, base + WREG + (wave * LWB + q - LWA) * 64, tvo[q], ic * p.HW * 4u);
+    else if (q < LWA + LWB) {
+      if constexpr (V4) dma16s(rsi, base + WREG + (wave * LWB + q - LWA) * 256, tvo[q], ic * p.HW * 4u);
+      else dma4s(rsi, base + WREG + (wave * LWB + q - LWA) * 64, tvo[q], ic * p.HW * 4u);
+    }
     else dma4(rsbias, base + WREG + SREG + 64 * wave, tvo[q]);
   };
 
@@ -151,9 +162,13 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
                                              rso, off, 0, AUX_OUT);
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dval[q][e]), rso,
+      for (int e = 0; e < 4; ++e) {
+        // (a scalar first: __builtin_bit_cast of a vector component made hipcc store component 0
+        // four times -- caught by the 224-wide, OH*OW % 4 == 2 test shapes)
+        const float xe = dval[q][e];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, xe), rso,
                                               oob_unless(px + (uint32_t)e < dhw, off + 4u * (uint32_t)e), 0, AUX_OUT);
+      }
     }
   };
 
@@ -241,7 +256,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     for (int tn = 0; tn < TN; ++tn) {
       const uint32_t px = p0 + (uint32_t)(wave * 32 * TN + 32 * tn + li);
       const uint32_t oy = fdiv(px, p.ow_m, p.ow_s), ox = px - oy * p.OW;
-      poff[tn] = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S) * 4u : 0u;
+      poff[tn] = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S + pxa - p.px) * 4u : 0u;
     }
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -326,10 +341,11 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #endif
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0>
 cfg_t dc_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 128 * TN, 2 * ((KY * KX + 1) / 2), 256, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D>;
+  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D, V4>;
+  c.dc_ci = V4;  // dc == 1: 16-B strip pieces (input rows of W % 4 == 0)
   c.dc = 1;
   c.dc_ky = KY;
   c.dc_kx = KX;
@@ -349,10 +365,16 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<7, 7, 2, 236, 13, 1, 2, 3>("dc7s2x32d3"),
       dc_cfg<7, 7, 2, 236, 13, 3, 2, 2>("dc7s2x96d2"),
       dc_cfg<7, 7, 2, 236, 11, 2, 1, 2>("dc7s2x64n128d2"),
+      dc_cfg<7, 7, 2, 236, 11, 2, 1, 2, 1>("dc7s2x64n128d2v"),
+      dc_cfg<7, 7, 2, 236, 13, 2, 2, 2, 1>("dc7s2x64d2v"),
+      dc_cfg<7, 7, 2, 236, 11, 2, 1, 3, 1>("dc7s2x64n128d3v"),
       // AlexNet conv1 (3 x 227^2 / 224^2 -> 96, 11x11 s4)
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2>("dc11s4x96d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2>("dc11s4x32d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3>("dc11s4x32d3"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 1>("dc11s4x32d2v"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 3, 1>("dc11s4x32d3v"),
+      dc_cfg<11, 11, 4, 228, 23, 3, 1, 2, 1>("dc11s4x96d2v"),
       // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
       dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
       dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),
@@ -365,7 +387,13 @@ int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY,
               uint32_t sx, bool first) {
   if ((int)KY != c.dc_ky || (int)KX != c.dc_kx || (int)sy != c.dc_s || (int)sx != c.dc_s)
     return bh::fail(BH_UNSUP, std::string("conv: direct config ") + c.name + " is for another kernel / stride");
-  if (p.W + 2 * p.px > (uint32_t)c.dc_wpm)
+  // strip columns: input x at column x + pxa; the rightmost tap column must exist (zero past W)
+  const bool v4 = c.dc_ci != 0;
+  if (v4 && (p.W % 4 || p.px > 4))
+    return bh::fail(BH_UNSUP, std::string("conv: 16-B strip pieces need W % 4 == 0, pad <= 4 for ") + c.name);
+  const uint32_t pxa = v4 ? (p.px ? 4u : 0u) : p.px;
+  const uint64_t maxcol = (uint64_t)pxa + (uint64_t)(p.OW - 1) * sx + KX - 1 - p.px;
+  if (pxa + p.W > (uint32_t)c.dc_wpm || maxcol >= (uint64_t)c.dc_wpm)
     return bh::fail(BH_UNSUP, std::string("conv: input row too wide for ") + c.name);
   const uint32_t npx = (uint32_t)c.BN, OW = p.OW, OHW = p.OHW;
   const uint32_t tiles = (OHW + npx - 1) / npx;

@@ -1170,6 +1170,11 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     // few output columns: stream the bank in its reference layout; the window covering the
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
     const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
+    if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
+      // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups
+      if (!k1 || IC % 16 || !avec) return fail(BH_UNSUP, "conv: gvo configs need a 1x1 conv with IC % 16 == 0");
+      return launch_gemm(ctx, 1, ch, A_MVEC, B_IM1X1S, p, "conv");
+    }
     if (avec)
       return launch_gemm(ctx, 1, ch, A_MVEC, fc ? B_FC : (k1 ? B_IM1X1 : B_IM2COL), p, "conv");
     ch = choice_t{};  // unaligned bank (K % 4 or pointer): a tile kernel

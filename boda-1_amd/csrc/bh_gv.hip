@@ -313,7 +313,11 @@ __device__ __forceinline__ typename fvec<R>::t ldv(__amdgpu_buffer_rsrc_t r, uin
 // registers)
 template <int R, int C, int NW, int NG, int DB, int BLD, int PD = 0>
 __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
-  static_assert(BLD == B_IMTAP || BLD == B_IM1X1S, "gvp loaders: one-tap im2col or 1x1");
+  // B_IM1X1 here: a 1x1 conv reading the bank in its reference layout (no packed bank): A rows
+  // of 16-B loads along k (lane group g holds k = k16 + 4 g .. + 3, step s takes k16 + 4 g + s:
+  // a quarter of the packed form's A loads at R = 1), B as B_IM1X1S with that k map
+  static_assert(BLD == B_IMTAP || BLD == B_IM1X1S || BLD == B_IM1X1, "gvp loaders: one-tap im2col or 1x1");
+  constexpr bool AO = BLD == B_IM1X1;
   using G = gv_geom<R, C, NW>;
   constexpr int BMr = G::BMr, NC = G::NC, KB = 16 * NG;
   typedef typename fvec<R>::t av_t;
@@ -334,6 +338,12 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   const uint32_t lda4 = p.lda * 4u, hw4 = p.HW * 4u;
   // A: channels m0 + R i .. (one R-aligned group of the OC4-padded row, or all past it)
   const uint32_t arow = oob_unless(m0 + R * i < p.lda, (m0 + R * i) * 4u + g * lda4);
+  uint32_t arow_o[AO ? R : 1];  // AO: row m0 + 16 r + i, k offset 4 g
+#pragma unroll
+  for (int r = 0; r < (AO ? R : 1); ++r) {
+    const uint32_t m = m0 + 16 * r + i;
+    arow_o[r] = oob_unless(m < p.M, (m * p.lda + 4 * g) * 4u);
+  }
   // B: per column tile, the lane's input pixel for channel g at tap (0, 0)
   uint32_t bcol[C];
   int iy0[C], ix0[C];
@@ -343,8 +353,8 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
     const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
     iy0[c] = 0;
     ix0[c] = 0;
-    if constexpr (BLD == B_IM1X1S) {
-      bcol[c] = oob_unless(n < p.N, (img * p.ICHW + pix + g * p.HW) * 4u);
+    if constexpr (BLD == B_IM1X1S || AO) {
+      bcol[c] = oob_unless(n < p.N, (img * p.ICHW + pix + (AO ? 4 * g : g) * p.HW) * 4u);
     } else {
       const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
       iy0[c] = (int)(oy * p.sy) - (int)p.py;
@@ -368,10 +378,23 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
     const bool live = k16 < kw1;  // wave-uniform
     const uint32_t av = live ? arow : OOB;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) a[s] = ldv<R>(rsa, av, (k16 + 4 * s) * lda4);
+    for (int s = 0; s < 4; ++s) {
+      if constexpr (!AO) a[s] = ldv<R>(rsa, av, (k16 + 4 * s) * lda4);
+    }
+    if constexpr (AO) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const f32x4v v = ld4(rsa, live ? arow_o[r] + k16 * 4u : OOB);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if constexpr (R == 1) a[s] = v[s];
+          else a[s][r] = v[s];
+        }
+      }
+    }
     uint32_t bv[C];
     uint32_t c0 = k16;
-    if constexpr (BLD == B_IM1X1S) {
+    if constexpr (BLD == B_IM1X1S || AO) {
 #pragma unroll
       for (int c = 0; c < C; ++c) bv[c] = live ? bcol[c] : OOB;
     } else {
@@ -388,7 +411,7 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int c = 0; c < C; ++c)
-        b[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (c0 + 4 * s) * hw4, 0));
+        b[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (AO ? c0 + s : c0 + 4 * s) * hw4, 0));
   };
   auto mma_grp = [&](const av_t(&a)[4], const float(&b)[4][C]) {
 #pragma unroll
@@ -462,7 +485,7 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   }
 
   KT(2);
-  gv_finish<R, C, NW, R>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
+  gv_finish<R, C, NW, AO ? 1 : R>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
 }
 
 template <int R, int C, int NW, int NG, int DB>
@@ -472,6 +495,15 @@ cfg_t gv_cfg(const char *name) {
   c.k[A_MVEC][B_FC][0] = gv_kernel<R, C, NW, NG, DB, B_FC>;
   c.k[A_MVEC][B_IM1X1][0] = gv_kernel<R, C, NW, NG, DB, B_IM1X1>;
   c.k[A_MVEC][B_IM2COL][0] = gv_kernel<R, C, NW, NG, DB, B_IM2COL>;
+  return c;
+}
+
+// gvo configurations: 1x1 convs over the bank in its reference layout (no pack), IC % 16 == 0
+template <int R, int C, int NW, int PD>
+cfg_t gvo_cfg(const char *name) {
+  cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 0};
+  c.gv = 1;
+  c.k[A_MVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, 1, 0, B_IM1X1, PD>;
   return c;
 }
 
@@ -543,6 +575,16 @@ std::vector<cfg_t> gv_cfgs() {
       gvp_cfg<4, 1, 16, 1, 0, 2>("gvs64x16w16"),
       gvp_cfg<1, 2, 16, 1, 0, 2>("gvs16x32w16"),
       gvp_cfg<4, 2, 4, 1, 0, 3>("gvs64x32"),
+      // 1x1 over the reference-layout bank (16-B A loads along k)
+      gvo_cfg<1, 1, 8, 3>("gvo16x16w8"),
+      gvo_cfg<1, 1, 16, 2>("gvo16x16w16"),
+      gvo_cfg<1, 2, 16, 2>("gvo16x32w16"),
+      gvo_cfg<2, 1, 16, 2>("gvo32x16w16"),
+      gvo_cfg<2, 2, 8, 3>("gvo32x32w8"),
+      gvo_cfg<2, 2, 16, 2>("gvo32x32w16"),
+      gvo_cfg<4, 2, 8, 2>("gvo64x32w8"),
+      gvo_cfg<4, 2, 16, 2>("gvo64x32w16"),
+      gvo_cfg<2, 4, 8, 2>("gvo32x64w8"),
   };
 }
 

@@ -35,7 +35,7 @@ CONV_SHAPES = [
 # direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py;
 # gvp* only IC % 16 == 0: test_conv_gvp below
 @pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1))
-                                if not n.startswith(("dc", "dm", "gvp", "gvs"))],
+                                if not n.startswith(("dc", "dm", "gvp", "gvs", "gvo"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):
@@ -149,7 +149,7 @@ GV_SHAPES = [
 
 
 @pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1)
-                                if n.startswith("gv") and not n.startswith(("gvp", "gvs"))])
+                                if n.startswith("gv") and not n.startswith(("gvp", "gvs", "gvo"))])
 @pytest.mark.parametrize("splits", [0, 1, 5])
 def test_conv_gv(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
@@ -206,5 +206,40 @@ def test_conv_gvp(dev, cn, splits):
             assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
         with pytest.raises(boda_hip.UnsupportedError):  # IC % 16 != 0
             run_conv(dev, ops.ConvShape(1, 24, 7, 7, 32, 3, 3, 1, 1, 1, 1))
+    finally:
+        dev.tune_set(1, -1, 0)
+
+
+# gvo*: 1x1 convs over the reference-layout bank (16-B A loads along k), IC % 16 == 0
+GVO_SHAPES = [s for s in GVP_SHAPES if s.KY == 1 and s.KX == 1] + [
+    ops.ConvShape(20, 528, 4, 4, 128, 1, 1, 1, 1, 0, 0),  # 320 columns over 20 images
+    ops.ConvShape(1, 1024, 7, 7, 50, 1, 1, 1, 1, 0, 0),   # long K, ragged M
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvo")])
+@pytest.mark.parametrize("splits", [0, 1, 3, 7])
+def test_conv_gvo(dev, cn, splits):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
+    try:
+        for s in GVO_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            ref = orc.conv_ref(i, f, b, s, 1)
+            nm, rl2, _ = orc.normalized_errors(ref, out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed-order combine
+            np.testing.assert_array_equal(run_conv(dev, s, packed=True), out)  # the pack is unused
+        rng = np.random.default_rng(11)
+        s = GVO_SHAPES[1]
+        hi = rng.standard_normal(s.B * s.IC * s.H * s.W).astype(np.float32)
+        hf = rng.standard_normal(s.OC * s.K).astype(np.float32)
+        hb = rng.standard_normal(s.OC).astype(np.float32)
+        out = run_conv(dev, s, host_inputs=(hi, hf, hb))
+        nm, rl2, _ = orc.normalized_errors(orc.conv_ref(hi, hf, hb, s, 1), out)
+        assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+        for bad in (ops.ConvShape(1, 32, 7, 7, 32, 3, 3, 1, 1, 1, 1), ops.ConvShape(1, 24, 7, 7, 32, 1, 1, 1, 1, 0, 0)):
+            with pytest.raises(boda_hip.UnsupportedError):  # not 1x1 / IC % 16 != 0
+                run_conv(dev, bad)
     finally:
         dev.tune_set(1, -1, 0)

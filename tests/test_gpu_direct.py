@@ -27,11 +27,14 @@ SHAPES = {
              ops.ConvShape(1, 3, 224, 224, 64, 7, 7, 2, 2, 3, 3),
              ops.ConvShape(3, 3, 227, 227, 96, 7, 7, 2, 2, 0, 0),
              ops.ConvShape(2, 1, 60, 41, 70, 7, 7, 2, 2, 1, 3),
-             ops.ConvShape(1, 4, 97, 100, 33, 7, 7, 2, 2, 2, 0)],
+             ops.ConvShape(1, 4, 97, 100, 33, 7, 7, 2, 2, 2, 0),
+             ops.ConvShape(2, 2, 40, 44, 20, 7, 7, 2, 2, 1, 1),    # W % 4 == 0, pad 1 (16-B strip)
+             ops.ConvShape(2, 3, 128, 128, 40, 7, 7, 2, 2, 3, 3)],  # W % 4 == 0, 2-row pixel tiles
     (11, 4): [ops.ConvShape(2, 3, 227, 227, 96, 11, 11, 4, 4, 0, 0),
               ops.ConvShape(1, 3, 224, 224, 96, 11, 11, 4, 4, 0, 0),
               ops.ConvShape(2, 2, 60, 71, 40, 11, 11, 4, 4, 2, 1),
-              ops.ConvShape(1, 4, 120, 100, 100, 11, 11, 4, 4, 5, 5)],
+              ops.ConvShape(1, 4, 120, 100, 100, 11, 11, 4, 4, 5, 5),
+              ops.ConvShape(1, 4, 100, 224, 40, 11, 11, 4, 4, 1, 1)],  # W % 4 == 0, pad 1 (16-B strip)
     (3, 1): [ops.ConvShape(1, 3, 224, 224, 64, 3, 3, 1, 1, 1, 1),
              ops.ConvShape(2, 3, 50, 210, 20, 3, 3, 1, 1, 1, 1),
              ops.ConvShape(1, 2, 40, 200, 70, 3, 3, 1, 1, 0, 2)],

@@ -164,7 +164,7 @@ def main():
                         cand += [(ci, 1), (ci, 2), (ci, 5), (ci, 6)]  # 5, 6: whole tiles per block
                         continue
                     if cn.startswith("gv"):  # register-streaming kernels: S = K chunks
-                        tm, tn = map(int, re.match(r"gv[pqs]?(\d+)x(\d+)", cn).groups())
+                        tm, tn = map(int, re.match(r"gv[pqso]?(\d+)x(\d+)", cn).groups())
                         tiles = -(-M // tm) * -(-N // tn)
                         if tiles <= 512:
                             cand += [(ci, S) for S in [0] + SPLITS if S == 0 or nkt >= S]
