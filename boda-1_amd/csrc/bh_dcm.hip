@@ -443,6 +443,15 @@ std::vector<cfg_t> dcm_cfgs() {
       dcm_cfg<5, 5, 32, 14, 0, 4, 2, 1, 2, 2>("dm5w32x128c4w8"),
       dcm_cfg<5, 5, 32, 14, 1, 4, 2, 1, 1, 2>("dm5w32vx64c4"),
       dcm_cfg<5, 5, 16, 20, 0, 4, 2, 1, 1, 2>("dm5w16x64c4"),
+      // 256-pixel tiles (TN = 2): half the filter-bank DMA per MFMA (the bank is re-fetched for
+      // every pixel tile: the largest cost left in the diagnostic builds)
+      dcm_cfg<3, 3, 16, 28, 0, 8, 2, 2, 2, 2>("dm3w16x128n256c8w8"),
+      dcm_cfg<3, 3, 16, 28, 0, 8, 2, 2, 1, 2>("dm3w16x64n256c8"),
+      dcm_cfg<3, 3, 8, 72, 0, 8, 2, 2, 2, 2>("dm3w8x128n256c8w8"),
+      dcm_cfg<3, 3, 32, 14, 1, 8, 2, 2, 1, 2>("dm3w32x64n256c8"),
+      dcm_cfg<3, 3, 60, 10, 1, 8, 2, 2, 1, 2>("dm3w60x64n256c8"),
+      dcm_cfg<5, 5, 32, 20, 0, 4, 2, 2, 1, 2>("dm5w32x64n256c4"),
+      dcm_cfg<5, 5, 32, 20, 0, 4, 2, 2, 2, 2>("dm5w32x128n256c4w8"),
       // 1x1: CI channels of the tile's 128 pixels per stage (16-B pieces when OH*OW % 4 == 0)
       dcm_cfg<1, 1, 0, 0, 1, 32, 2, 1, 1, 3>("dm1vx64c32"),
       dcm_cfg<1, 1, 0, 0, 1, 32, 2, 1, 2, 3>("dm1vx128c32w8"),
