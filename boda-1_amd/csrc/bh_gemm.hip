@@ -1173,6 +1173,8 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
       // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups
       if (!k1 || IC % 16 || !avec) return fail(BH_UNSUP, "conv: gvo configs need a 1x1 conv with IC % 16 == 0");
+      if ((OH * OW) % (uint32_t)cfgs(1)[ch.cfg].gv_cx)
+        return fail(BH_UNSUP, "conv: interleaved-column configs need OH*OW % run == 0");
       return launch_gemm(ctx, 1, ch, A_MVEC, B_IM1X1S, p, "conv");
     }
     if (avec)
@@ -1213,6 +1215,8 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
         // register streaming over the packed bank (bh_gv.hip gvp_kernel): 16-deep k groups
         // inside one filter tap
         if (IC % 16) return fail(BH_UNSUP, "conv: gvp configs need IC % 16 == 0");
+        if (cfgs(1)[ch.cfg].gv_cx > 1 && (!k1 || (OH * OW) % (uint32_t)cfgs(1)[ch.cfg].gv_cx))
+          return fail(BH_UNSUP, "conv: interleaved-column configs need a 1x1 conv with OH*OW % run == 0");
         return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1S : B_IMTAP, p, "conv", packed != nullptr);
       }
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;

@@ -56,7 +56,8 @@ __device__ __forceinline__ void gv_bias(const GemmArgs &p, uint32_t m0, int tid,
 // slabs in chunk order (the split-K protocol of bh_gemm.hip: bitwise reproducible).
 // RS: row interleave of the MFMA row tiles -- row rho of tile r is block row RS * rho + r
 // (RS = 1: tile r owns rows 16 r .. 16 r + 15, written as 16 r + rho).
-template <int R, int C, int NW, int RS>
+// CX > 1: column tiles interleaved -- column i of MFMA tile c is block column CX * i + c
+template <int R, int C, int NW, int RS, int CX = 1>
 __device__ __forceinline__ void gv_finish(const GemmArgs &p, f32x4t (&acc)[R][C], float *red, uint32_t tm, uint32_t tn,
                                           int tid, int wave, int lane,
                                           const float (&bias_r)[gv_geom<R, C, NW>::CH]) {
@@ -75,7 +76,7 @@ __device__ __forceinline__ void gv_finish(const GemmArgs &p, f32x4t (&acc)[R][C]
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = RS == 1 ? 16 * r + 4 * g + j : RS * (4 * g + j) + r;
-          Rw[row * NC + 16 * c + i] = acc[r][c][j];
+          Rw[row * NC + (CX > 1 ? CX * i + c : 16 * c + i)] = acc[r][c][j];
         }
   }
   __syncthreads();
@@ -311,13 +312,18 @@ __device__ __forceinline__ typename fvec<R>::t ldv(__amdgpu_buffer_rsrc_t r, uin
 // group g + PD are issued before group g's MFMAs, so PD groups of loads are always in flight
 // (the batch form with DB = 0 exposes a whole memory round trip per batch; DB = 1 doubles its
 // registers)
-template <int R, int C, int NW, int NG, int DB, int BLD, int PD = 0>
+// CX = C (2 or 4, 1x1 only, OH*OW % CX == 0): the C column tiles are interleaved, so a lane's
+// CX consecutive pixels are ONE CX-wide load per k (column i of tile c = pixel CX * i + c):
+// a quarter / half of the B load instructions -- on small ops the loads a CU must issue
+// through its address unit, not their bytes, set the time to the first MFMA
+template <int R, int C, int NW, int NG, int DB, int BLD, int PD = 0, int CX = 1>
 __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   // B_IM1X1 here: a 1x1 conv reading the bank in its reference layout (no packed bank): A rows
   // of 16-B loads along k (lane group g holds k = k16 + 4 g .. + 3, step s takes k16 + 4 g + s:
   // a quarter of the packed form's A loads at R = 1), B as B_IM1X1S with that k map
   static_assert(BLD == B_IMTAP || BLD == B_IM1X1S || BLD == B_IM1X1, "gvp loaders: one-tap im2col or 1x1");
   constexpr bool AO = BLD == B_IM1X1;
+  static_assert(CX == 1 || (CX == C && (CX == 2 || CX == 4) && BLD != B_IMTAP), "column interleave: 1x1, CX == C");
   using G = gv_geom<R, C, NW>;
   constexpr int BMr = G::BMr, NC = G::NC, KB = 16 * NG;
   typedef typename fvec<R>::t av_t;
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   int iy0[C], ix0[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    const uint32_t n = tn * NC + 16 * c + i;
+    const uint32_t n = CX > 1 ? tn * NC + CX * i : tn * NC + 16 * c + i;  // CX > 1: the lane's run
     const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
     iy0[c] = 0;
     ix0[c] = 0;
@@ -407,11 +413,20 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
         bv[c] = oob_unless(ok, (uint32_t)((int)bcol[c] + (int)(ky * p.W + kx)) * 4u);
       }
     }
+    if constexpr (CX > 1) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const typename fvec<CX>::t v = ldv<CX>(rsb, bv[0], (AO ? c0 + s : c0 + 4 * s) * hw4);
+#pragma unroll
+        for (int c = 0; c < C; ++c) b[s][c] = v[c];
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int c = 0; c < C; ++c)
         b[s][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, bv[c], (AO ? c0 + s : c0 + 4 * s) * hw4, 0));
+    }
   };
   auto mma_grp = [&](const av_t(&a)[4], const float(&b)[4][C]) {
 #pragma unroll
@@ -485,7 +500,7 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   }
 
   KT(2);
-  gv_finish<R, C, NW, AO ? 1 : R>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
+  gv_finish<R, C, NW, AO ? 1 : R, CX>(p, acc, red, tm, tn, tid, wave, lane, bias_r);
 }
 
 template <int R, int C, int NW, int NG, int DB>
@@ -499,11 +514,21 @@ cfg_t gv_cfg(const char *name) {
 }
 
 // gvo configurations: 1x1 convs over the bank in its reference layout (no pack), IC % 16 == 0
-template <int R, int C, int NW, int PD>
+template <int R, int C, int NW, int PD, int CX = 1>
 cfg_t gvo_cfg(const char *name) {
   cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 0};
   c.gv = 1;
-  c.k[A_MVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, 1, 0, B_IM1X1, PD>;
+  c.gv_cx = CX;
+  c.k[A_MVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, 1, 0, B_IM1X1, PD, CX>;
+  return c;
+}
+// gvs over the packed bank with interleaved column tiles (1x1 only)
+template <int R, int C, int NW, int PD, int CX>
+cfg_t gvx_cfg(const char *name) {
+  cfg_t c{name, 16 * R, 16 * C, 16 * NW, NW * 64, {}, 1};
+  c.gv = 1;
+  c.gv_cx = CX;
+  c.k[A_KVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, 1, 0, B_IM1X1S, PD, CX>;
   return c;
 }
 
@@ -585,6 +610,15 @@ std::vector<cfg_t> gv_cfgs() {
       gvo_cfg<4, 2, 8, 2>("gvo64x32w8"),
       gvo_cfg<4, 2, 16, 2>("gvo64x32w16"),
       gvo_cfg<2, 4, 8, 2>("gvo32x64w8"),
+      // interleaved column tiles: one 8-B / 16-B pixel-run load per k (1x1, OH*OW % CX == 0)
+      gvo_cfg<1, 4, 8, 3, 4>("gvo16x64xw8"),
+      gvo_cfg<1, 4, 16, 2, 4>("gvo16x64xw16"),
+      gvo_cfg<1, 2, 16, 2, 2>("gvo16x32xw16"),
+      gvo_cfg<2, 4, 8, 2, 4>("gvo32x64xw8"),
+      gvo_cfg<2, 2, 16, 2, 2>("gvo32x32xw16"),
+      gvx_cfg<4, 4, 8, 2, 4>("gvs64x64xw8"),
+      gvx_cfg<2, 4, 16, 2, 4>("gvs32x64xw16"),
+      gvx_cfg<4, 2, 16, 2, 2>("gvs64x32xw16"),
   };
 }
 

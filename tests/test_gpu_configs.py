@@ -181,7 +181,7 @@ GVP_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("gvp", "gvs"))])
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("gvp", "gvs")) and "xw" not in n])
 @pytest.mark.parametrize("splits", [0, 1, 3, 7])
 def test_conv_gvp(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
@@ -217,7 +217,7 @@ GVO_SHAPES = [s for s in GVP_SHAPES if s.KY == 1 and s.KX == 1] + [
 ]
 
 
-@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvo")])
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvo") and "xw" not in n])
 @pytest.mark.parametrize("splits", [0, 1, 3, 7])
 def test_conv_gvo(dev, cn, splits):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
@@ -240,6 +240,44 @@ def test_conv_gvo(dev, cn, splits):
         assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
         for bad in (ops.ConvShape(1, 32, 7, 7, 32, 3, 3, 1, 1, 1, 1), ops.ConvShape(1, 24, 7, 7, 32, 1, 1, 1, 1, 0, 0)):
             with pytest.raises(boda_hip.UnsupportedError):  # not 1x1 / IC % 16 != 0
+                run_conv(dev, bad)
+    finally:
+        dev.tune_set(1, -1, 0)
+
+
+# interleaved column tiles (names *xw*: column i of MFMA tile c = pixel run position CX*i + c; one
+# CX-wide load per k): 1x1 convs with OH*OW % CX == 0
+GVX_SHAPES = [
+    ops.ConvShape(2, 64, 14, 14, 96, 1, 1, 1, 1, 0, 0),
+    ops.ConvShape(3, 96, 6, 6, 70, 1, 1, 1, 1, 0, 0),      # ragged M, 108 columns
+    ops.ConvShape(20, 528, 4, 4, 128, 1, 1, 1, 1, 0, 0),
+    ops.ConvShape(1, 512, 14, 14, 50, 1, 1, 1, 1, 0, 0),   # long K, 196 columns (ragged last tile)
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gv") and "xw" in n])
+@pytest.mark.parametrize("splits", [0, 1, 3])
+def test_conv_gv_interleaved(dev, cn, splits):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
+    try:
+        for s in GVX_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            nm, rl2, _ = orc.normalized_errors(orc.conv_ref(i, f, b, s, 1), out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)
+            np.testing.assert_array_equal(run_conv(dev, s, packed=True), out)
+        rng = np.random.default_rng(5)
+        s = GVX_SHAPES[1]
+        hi = rng.standard_normal(s.B * s.IC * s.H * s.W).astype(np.float32)
+        hf = rng.standard_normal(s.OC * s.K).astype(np.float32)
+        hb = rng.standard_normal(s.OC).astype(np.float32)
+        out = run_conv(dev, s, host_inputs=(hi, hf, hb))
+        nm, rl2, _ = orc.normalized_errors(orc.conv_ref(hi, hf, hb, s, 1), out)
+        assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+        for bad in (ops.ConvShape(5, 832, 7, 7, 48, 1, 1, 1, 1, 0, 0),   # OH*OW = 49
+                    ops.ConvShape(1, 32, 8, 8, 32, 3, 3, 1, 1, 1, 1)):   # not 1x1
+            with pytest.raises(boda_hip.UnsupportedError):
                 run_conv(dev, bad)
     finally:
         dev.tune_set(1, -1, 0)
