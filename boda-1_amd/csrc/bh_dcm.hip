@@ -458,6 +458,12 @@ std::vector<cfg_t> dcm_cfgs() {
       dcm_cfg<1, 1, 0, 0, 1, 16, 2, 1, 1, 4>("dm1vx64c16"),
       dcm_cfg<1, 1, 0, 0, 0, 32, 2, 1, 1, 3>("dm1x64c32"),
       dcm_cfg<1, 1, 0, 0, 0, 32, 2, 1, 2, 3>("dm1x128c32w8"),
+      // short-K 1x1 (K = 64 / 96 / 128): the whole K, or half, in one stage -- one barrier per
+      // tile, the ring runs across tiles
+      dcm_cfg<1, 1, 0, 0, 1, 64, 2, 1, 1, 2>("dm1vx64c64"),
+      dcm_cfg<1, 1, 0, 0, 1, 64, 2, 1, 1, 3>("dm1vx64c64d3"),
+      dcm_cfg<1, 1, 0, 0, 1, 96, 2, 1, 1, 2>("dm1vx64c96"),
+      dcm_cfg<1, 1, 0, 0, 1, 64, 2, 1, 2, 2>("dm1vx128c64w8"),
 #ifdef BH_KTRACE
       // diagnostic builds (instrumented library only; wrong results by design)
       dcm_cfg<3, 3, 16, 16, 0, 8, 2, 1, 1, 2, 1>("xdm3w16x64c8_nodma"),
