@@ -1171,7 +1171,10 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
     const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
     if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
-      // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups
+      // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups; an ipconv takes
+      // its input rows as the columns (B_FC, one 16-B load per column tile and k group)
+      if (fc && K % 16 == 0 && avec && cfgs(1)[ch.cfg].k[A_MVEC][B_FC][0])
+        return launch_gemm(ctx, 1, ch, A_MVEC, B_FC, p, "conv");
       if (!k1 || IC % 16 || !avec) return fail(BH_UNSUP, "conv: gvo configs need a 1x1 conv with IC % 16 == 0");
       if ((OH * OW) % (uint32_t)cfgs(1)[ch.cfg].gv_cx)
         return fail(BH_UNSUP, "conv: interleaved-column configs need OH*OW % run == 0");

@@ -321,8 +321,11 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
   // B_IM1X1 here: a 1x1 conv reading the bank in its reference layout (no packed bank): A rows
   // of 16-B loads along k (lane group g holds k = k16 + 4 g .. + 3, step s takes k16 + 4 g + s:
   // a quarter of the packed form's A loads at R = 1), B as B_IM1X1S with that k map
-  static_assert(BLD == B_IMTAP || BLD == B_IM1X1S || BLD == B_IM1X1, "gvp loaders: one-tap im2col or 1x1");
-  constexpr bool AO = BLD == B_IM1X1;
+  // B_FC: an ipconv (window = whole input, OH = OW = 1, K % 16 == 0) over the reference-layout
+  // bank: A as B_IM1X1, B = in[n * K + k] one 16-B load per column tile along the same k map
+  static_assert(BLD == B_IMTAP || BLD == B_IM1X1S || BLD == B_IM1X1 || BLD == B_FC,
+                "gvp loaders: one-tap im2col, 1x1 or ipconv");
+  constexpr bool AO = BLD == B_IM1X1 || BLD == B_FC;
   static_assert(CX == 1 || (CX == C && (CX == 2 || CX == 4) && BLD != B_IMTAP), "column interleave: 1x1, CX == C");
   using G = gv_geom<R, C, NW>;
   constexpr int BMr = G::BMr, NC = G::NC, KB = 16 * NG;
@@ -359,7 +362,9 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
     const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
     iy0[c] = 0;
     ix0[c] = 0;
-    if constexpr (BLD == B_IM1X1S || AO) {
+    if constexpr (BLD == B_FC) {
+      bcol[c] = oob_unless(n < p.N, (n * p.ICHW + 4 * g) * 4u);
+    } else if constexpr (BLD == B_IM1X1S || AO) {
       bcol[c] = oob_unless(n < p.N, (img * p.ICHW + pix + (AO ? 4 * g : g) * p.HW) * 4u);
     } else {
       const uint32_t oy = fdiv(pix, p.ow_m, p.ow_s), ox = pix - oy * p.OW;
@@ -413,7 +418,14 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
         bv[c] = oob_unless(ok, (uint32_t)((int)bcol[c] + (int)(ky * p.W + kx)) * 4u);
       }
     }
-    if constexpr (CX > 1) {
+    if constexpr (BLD == B_FC) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const f32x4v v = ld4(rsb, live ? bcol[c] + k16 * 4u : OOB);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s][c] = v[s];
+      }
+    } else if constexpr (CX > 1) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const typename fvec<CX>::t v = ldv<CX>(rsb, bv[0], (AO ? c0 + s : c0 + 4 * s) * hw4);
@@ -520,6 +532,7 @@ cfg_t gvo_cfg(const char *name) {
   c.gv = 1;
   c.gv_cx = CX;
   c.k[A_MVEC][B_IM1X1S][0] = gvp_kernel<R, C, NW, 1, 0, B_IM1X1, PD, CX>;
+  if constexpr (CX == 1) c.k[A_MVEC][B_FC][0] = gvp_kernel<R, C, NW, 1, 0, B_FC, PD>;
   return c;
 }
 // gvs over the packed bank with interleaved column tiles (1x1 only)

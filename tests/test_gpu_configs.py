@@ -245,6 +245,42 @@ def test_conv_gvo(dev, cn, splits):
         dev.tune_set(1, -1, 0)
 
 
+# gvo* on ipconv / FC ops (window = the whole unpadded input, OH = OW = 1, K % 16 == 0): the
+# input rows are the columns (B_FC, one 16-B load per column tile and k group)
+GVO_FC_SHAPES = [
+    ops.ConvShape(4, 256, 6, 6, 130, 6, 6, 1, 1, 0, 0),   # fc6-like, K 9216, ragged M
+    ops.ConvShape(20, 64, 1, 1, 100, 1, 1, 1, 1, 0, 0),   # 1x1 over a 1x1 input, 20 columns
+    ops.ConvShape(3, 128, 4, 4, 70, 4, 4, 1, 1, 0, 0),    # K 2048
+    ops.ConvShape(1, 1024, 1, 1, 1000, 1, 1, 1, 1, 0, 0), # one column
+    ops.ConvShape(17, 48, 2, 2, 33, 2, 2, 1, 1, 0, 0),    # K 192, ragged N and M
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("gvo") and "xw" not in n])
+@pytest.mark.parametrize("splits", [0, 1, 4])
+def test_conv_gvo_ipconv(dev, cn, splits):
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), splits)
+    try:
+        for s in GVO_FC_SHAPES:
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            nm, rl2, _ = orc.normalized_errors(orc.conv_ref(i, f, b, s, 1), out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed-order combine
+        rng = np.random.default_rng(13)
+        for s in (GVO_FC_SHAPES[0], GVO_FC_SHAPES[4]):
+            hi = rng.standard_normal(s.B * s.IC * s.H * s.W).astype(np.float32)
+            hf = rng.standard_normal(s.OC * s.K).astype(np.float32)
+            hb = rng.standard_normal(s.OC).astype(np.float32)
+            out = run_conv(dev, s, host_inputs=(hi, hf, hb))
+            nm, rl2, _ = orc.normalized_errors(orc.conv_ref(hi, hf, hb, s, 1), out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+        with pytest.raises(boda_hip.UnsupportedError):  # ipconv with K % 16 != 0
+            run_conv(dev, ops.ConvShape(2, 5, 2, 2, 8, 2, 2, 1, 1, 0, 0))
+    finally:
+        dev.tune_set(1, -1, 0)
+
+
 # interleaved column tiles (names *xw*: column i of MFMA tile c = pixel run position CX*i + c; one
 # CX-wide load per k): 1x1 convs with OH*OW % CX == 0
 GVX_SHAPES = [

@@ -90,6 +90,36 @@ int code_run(const char *name, F launch, unsigned long long *marks, hipStream_t 
   return 0;
 }
 
+// load-issue rate: each lane issues NL independent loads of W dwords (all in flight), 8 waves a
+// block, one block per CU; in-kernel span from the first entry to the last completion
+template <int NL, int W>
+__global__ __launch_bounds__(512) void issue_k(const float *in, float *out, unsigned long long *marks, int launch) {
+  const int tid = threadIdx.x;
+  const unsigned long long t0 = wall_clock64();
+  float s = 0.0f;
+  const float *base = in + (size_t)blockIdx.x * (NL * 512 * W);
+  if constexpr (W == 1) {
+    float v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) v[j] = base[j * 512 + tid];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) s += v[j];
+  } else {
+    float4 v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) v[j] = ((const float4 *)base)[j * 512 + tid];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) s += v[j].x + v[j].y + v[j].z + v[j].w;
+  }
+  out[(size_t)blockIdx.x * 512 + tid] = s;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t1 = wall_clock64();
+  if (tid == 0) {
+    marks[((size_t)launch * gridDim.x + blockIdx.x) * 4] = t0;
+    marks[((size_t)launch * gridDim.x + blockIdx.x) * 4 + 1] = t1;
+  }
+}
+
 int main() {
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -151,6 +181,18 @@ int main() {
     }
     CK(hipGraphExecDestroy(ge));
     CK(hipGraphDestroy(g));
+  }
+  {
+    float *big;
+    CK(hipMalloc(&big, (size_t)256 * 64 * 512 * 16));
+    CK(hipMemset(big, 0, (size_t)256 * 64 * 512 * 16));
+    float *o2;
+    CK(hipMalloc(&o2, 256 * 512 * 4));
+    if (code_run("8 dword loads/lane, 8 waves", [&](int l) { issue_k<8, 1><<<256, 512, 0, st>>>(big, o2, marks, l); }, marks, st, 256)) return 1;
+    if (code_run("32 dword loads/lane, 8 waves", [&](int l) { issue_k<32, 1><<<256, 512, 0, st>>>(big, o2, marks, l); }, marks, st, 256)) return 1;
+    if (code_run("64 dword loads/lane, 8 waves", [&](int l) { issue_k<64, 1><<<256, 512, 0, st>>>(big, o2, marks, l); }, marks, st, 256)) return 1;
+    if (code_run("8 dwordx4 loads/lane, 8 waves", [&](int l) { issue_k<8, 4><<<256, 512, 0, st>>>(big, o2, marks, l); }, marks, st, 256)) return 1;
+    if (code_run("32 dwordx4 loads/lane, 8 waves", [&](int l) { issue_k<32, 4><<<256, 512, 0, st>>>(big, o2, marks, l); }, marks, st, 256)) return 1;
   }
   for (int blocks : {1, 256}) {
     if (code_run("4096 s_nop straight-line (16 KB)", [&](int l) { code_big<<<blocks, 64, 0, st>>>(marks, l); }, marks, st,
