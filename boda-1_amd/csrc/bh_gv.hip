@@ -473,9 +473,13 @@ __global__ __launch_bounds__(NW * 64) void gvp_kernel(GemmArgs p) {
       for (int r = 0; r < RING; ++r) step(r, k + 16u * r);
       if (g == 0) KT(1);
     }
+    // tail: < RING groups left, all already in flight -- MFMAs only (no dead prefetches)
 #pragma unroll
     for (int r = 0; r < RING - 1; ++r)
-      if (g + r < ngrp) step(r, k + 16u * r);
+      if (g + r < ngrp) {
+        __builtin_amdgcn_sched_barrier(0);
+        mma_grp(ra[r % RING], rb[r % RING]);
+      }
   } else {
   av_t a0[NG][4], a1[DB ? NG : 1][4];
   float b0[NG][4][C], b1[DB ? NG : 1][4][C];
