@@ -1070,6 +1070,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
   if (c.streamk) return s + "_streamk";
   if (c.dc == 2) return std::string("mfma32_conv_dm_") + c.name;
   if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
+  if (c.fcv) return std::string("conv_fcv_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
   uint32_t S = resolve_splits(c, ch, M, N, K, 256);
   if (S > 1) {
@@ -1170,6 +1171,16 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     // few output columns: stream the bank in its reference layout; the window covering the
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
     const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
+    if (cfgs(1)[ch.cfg].fcv) {
+      // batch-streaming ipconv (bh_gv.hip fcv_kernel): a wave per BM / 4 bank rows
+      const cfg_t &fc_c = cfgs(1)[ch.cfg];
+      if (!fc || !avec || B > (uint32_t)fc_c.BN)
+        return fail(BH_UNSUP, "conv: fcv configs need an ipconv (window = the whole unpadded input) at batch <= " +
+                                  std::to_string(fc_c.BN) + " with K % 4 == 0");
+      void *args[] = {&p};
+      return bh::launch(ctx, (const void *)fc_c.k[A_MVEC][B_FC][0], dim3((OC + fc_c.BM - 1) / fc_c.BM), dim3(256), args,
+                        true, true, "conv");
+    }
     if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
       // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups; an ipconv takes
       // its input rows as the columns (B_FC, one 16-B load per column tile and k group)

@@ -334,6 +334,7 @@ struct cfg_t {
   int dc_ky = 0, dc_kx = 0, dc_s = 0, dc_wpm = 0, dc_rin = 0;
   int dc_ci = 0;      // dc == 2 (bh_dcm.hip): input channels per stage
   int gv_cx = 1;      // gv: interleaved column tiles (1x1, a lane's gv_cx pixels per load)
+  int fcv = 0;        // gv: batch-streaming ipconv kernel (bh_gv.hip fcv_kernel), batch <= BN
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and

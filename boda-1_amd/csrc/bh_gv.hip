@@ -529,6 +529,81 @@ cfg_t gv_cfg(const char *name) {
   return c;
 }
 
+// fcv_kernel: ipconv / FC ops at batch N <= NB (a matrix-vector product per image): the op is
+// one read of the bank, and the MFMA tiles waste 15/16 of their columns at N = 1 while their
+// operand loads cover 16 rows x 64 B each. Here a wave owns R output channels (bank rows) and
+// streams them along k, one 16-B piece per lane -- each load instruction is 1 KB of ONE row, as
+// the contiguous stream that reaches HBM peak in tools/lat_bench.hip -- with U pieces per row
+// in flight; the N input rows come in the same k pieces (L2-resident: K * N * 4 bytes), the
+// products are summed per lane (fmaf chain over the lane's k, in k order), then across the wave
+// by a butterfly, and R x N lanes store the results (bias, residual, ReLU as finish_store_b).
+template <int R, int U, int NB>
+__global__ __launch_bounds__(256) void fcv_kernel(GemmArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t m0 = (blockIdx.x * 4u + (uint32_t)wave) * R;
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.b, p.b_bytes);
+  const uint32_t K = p.K;
+  uint32_t wrow[R], xrow[NB];
+#pragma unroll
+  for (int r = 0; r < R; ++r) wrow[r] = m0 + r < p.M ? (m0 + r) * K * 4u + 16u * lane : OOB;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) xrow[b] = (uint32_t)b < p.N ? (uint32_t)b * p.ICHW * 4u + 16u * lane : OOB;
+  float acc[R][NB];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[r][b] = 0.0f;
+  for (uint32_t kc = 0; kc < K; kc += 256u * U) {
+    f32x4v w[U][R], x[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = kc + 256u * u + 4u * lane < K;  // (K % 4 == 0: a piece is whole or past the row)
+      const uint32_t ko = (kc + 256u * u) * 4u;
+#pragma unroll
+      for (int r = 0; r < R; ++r) w[u][r] = ld4(rsa, live ? wrow[r] + ko : OOB);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) x[u][b] = ld4(rsb, live ? xrow[b] + ko : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[r][b] = __builtin_fmaf(w[u][r][e], x[u][b][e], acc[r][b]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc[r][b] += __shfl_xor(acc[r][b], o, 64);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t m = m0 + r;
+      if (lane == r * NB + b && m < p.M && (uint32_t)b < p.N) {
+        const size_t o = (size_t)b * p.OCOHW + m;
+        float v = acc[r][b] + (p.bias ? p.bias[m] : 0.0f);
+        if (p.res) v += p.res[o];
+        p.c[o] = (p.relu && v < 0.0f) ? 0.0f : v;
+      }
+    }
+}
+
+template <int R, int U, int NB>
+cfg_t fcv_cfg(const char *name) {
+  cfg_t c{name, 4 * R, NB, 256 * U, 256, {}, 0};
+  c.gv = 1;
+  c.fcv = 1;
+  c.k[A_MVEC][B_FC][0] = fcv_kernel<R, U, NB>;
+  return c;
+}
+
 // gvo configurations: 1x1 convs over the bank in its reference layout (no pack), IC % 16 == 0
 template <int R, int C, int NW, int PD, int CX = 1>
 cfg_t gvo_cfg(const char *name) {
@@ -627,6 +702,12 @@ std::vector<cfg_t> gv_cfgs() {
       gvo_cfg<4, 2, 8, 2>("gvo64x32w8"),
       gvo_cfg<4, 2, 16, 2>("gvo64x32w16"),
       gvo_cfg<2, 4, 8, 2>("gvo32x64w8"),
+      // batch-streaming ipconv (batch <= 1 / 2 / 4; batch-5 variants measured slower than gv)
+      fcv_cfg<2, 8, 1>("fcv2u8n1"),
+      fcv_cfg<4, 4, 1>("fcv4u4n1"),
+      fcv_cfg<1, 16, 1>("fcv1u16n1"),
+      fcv_cfg<2, 4, 2>("fcv2u4n2"),
+      fcv_cfg<4, 4, 4>("fcv4u4n4"),
       // interleaved column tiles: one 8-B / 16-B pixel-run load per k (1x1, OH*OW % CX == 0)
       gvo_cfg<1, 4, 8, 3, 4>("gvo16x64xw8"),
       gvo_cfg<1, 4, 16, 2, 4>("gvo16x64xw16"),

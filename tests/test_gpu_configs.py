@@ -5,6 +5,8 @@ configuration, so each one is checked on shapes that exercise ragged M/N/K
 edges, both A loaders (K % 4 == 0 or not) and both B loaders (1x1 and im2col).
 Tolerances as in test_gpu_conv.py.
 """
+import re
+
 import numpy as np
 import pytest
 
@@ -35,7 +37,7 @@ CONV_SHAPES = [
 # direct-conv configs (dc*) serve only their own kernel size / stride: tests/test_gpu_direct.py;
 # gvp* only IC % 16 == 0: test_conv_gvp below
 @pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1))
-                                if not n.startswith(("dc", "dm", "gvp", "gvs", "gvo"))],
+                                if not n.startswith(("dc", "dm", "gvp", "gvs", "gvo", "fcv"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):
@@ -279,6 +281,49 @@ def test_conv_gvo_ipconv(dev, cn, splits):
             run_conv(dev, ops.ConvShape(2, 5, 2, 2, 8, 2, 2, 1, 1, 0, 0))
     finally:
         dev.tune_set(1, -1, 0)
+
+
+# fcv*: batch-streaming ipconv (a wave per bank rows, lanes along k; batch <= the config's n<NB>)
+FCV_SHAPES = [
+    ops.ConvShape(1, 256, 6, 6, 130, 6, 6, 1, 1, 0, 0),   # fc6-like, K 9216, ragged M
+    ops.ConvShape(1, 4096, 1, 1, 1000, 1, 1, 1, 1, 0, 0), # fc8-like
+    ops.ConvShape(1, 12, 3, 3, 37, 3, 3, 1, 1, 0, 0),     # K 108: a partial 256-k chunk
+    ops.ConvShape(2, 128, 4, 4, 70, 4, 4, 1, 1, 0, 0),    # K 2048, batch 2
+    ops.ConvShape(4, 1000, 1, 1, 33, 1, 1, 1, 1, 0, 0),   # batch 4, K % 256 != 0
+    ops.ConvShape(5, 64, 2, 2, 50, 2, 2, 1, 1, 0, 0),     # batch 5
+]
+
+
+@pytest.mark.parametrize("cn", [n for n in boda_hip.tune_cfg_names(1) if n.startswith("fcv")])
+def test_conv_fcv(dev, cn):
+    nb = int(re.search(r"n(\d+)$", cn).group(1))
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
+    ran = 0
+    try:
+        for s in FCV_SHAPES:
+            if s.B > nb:
+                with pytest.raises(boda_hip.UnsupportedError):  # batch past the config's
+                    run_conv(dev, s)
+                continue
+            ran += 1
+            out = run_conv(dev, s)
+            i, f, b = orc.gen_conv(s, 5)
+            nm, rl2, _ = orc.normalized_errors(orc.conv_ref(i, f, b, s, 1), out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+            np.testing.assert_array_equal(run_conv(dev, s), out)  # fixed summation order
+            hi = np.random.default_rng(17).standard_normal(s.B * s.IC * s.H * s.W).astype(np.float32)
+            hf = np.random.default_rng(18).standard_normal(s.OC * s.K).astype(np.float32)
+            hb = np.random.default_rng(19).standard_normal(s.OC).astype(np.float32)
+            out = run_conv(dev, s, host_inputs=(hi, hf, hb))
+            nm, rl2, _ = orc.normalized_errors(orc.conv_ref(hi, hf, hb, s, 1), out)
+            assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+        for bad in (ops.ConvShape(1, 32, 7, 7, 32, 3, 3, 1, 1, 1, 1),   # not an ipconv
+                    ops.ConvShape(1, 16, 4, 4, 8, 4, 4, 1, 1, 1, 1)):   # padded window
+            with pytest.raises(boda_hip.UnsupportedError):
+                run_conv(dev, bad)
+    finally:
+        dev.tune_set(1, -1, 0)
+    assert ran >= 3
 
 
 # interleaved column tiles (names *xw*: column i of MFMA tile c = pixel run position CX*i + c; one

@@ -41,7 +41,7 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
-    if name.startswith(("dc", "dm")):
+    if name.startswith(("dc", "dm", "fcv")):
         return 1 << 30
     if name.startswith("gv"):
         m = re.search(r"w(\d+)", name)
@@ -159,6 +159,9 @@ def main():
                     if cn.startswith("dc"):  # direct conv (stems): no K split; UNSUP for other kernels
                         if kind == 1 and cn.startswith("dc%ds%d" % (s.KY, s.sy)) and s.KX == s.KY and s.sx == s.sy:
                             cand.append((ci, 0))
+                        continue
+                    if cn.startswith("fcv"):  # batch-streaming ipconv: no K split; UNSUP for other ops
+                        cand.append((ci, 0))
                         continue
                     if cn.startswith("srk"):  # stream-K: S = blocks per CU
                         cand += [(ci, 1), (ci, 2), (ci, 5), (ci, 6)]  # 5, 6: whole tiles per block
