@@ -79,14 +79,35 @@ def shard_units(shapes, tags, world, rank):
     return units, [units[i] for i in parts[rank]], pred
 
 
+def cpu_info():
+    """Host facts for the CPU baseline line: logical CPUs, the CPUs this process may run on, the
+    CPU model string."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for l in f:
+                if l.startswith("model name"):
+                    model = l.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity": aff, "cpu_model": model}
+
+
 def cpu_baseline(budget_s):
-    """Time the oracle's fp32 OpenMP CPU path on a bounded sample of the same workload."""
+    """Time the oracle's fp32 OpenMP CPU path on a bounded sample of the same workload: every op
+    of conv-ops-1-5-20 and op_sigs_full, then the SGEMMs of sgemm-ops-small/full smallest first
+    until the time budget is spent."""
     from oracle import oracle as orc
     conv, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["conv"]))
+    sigs, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["op-sigs"]))
     sg, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["sgemm-small"]))
     sgf, _ = ops.read_ops(os.path.join(OPS_DIR, SETS["sgemm-full"]))
-    # every conv op, then the SGEMMs smallest first until the time budget is spent
-    sample = [ops.shape_of(o) for o in conv]
+    sample = [ops.shape_of(o) for o in conv] + [ops.shape_of(o) for o in sigs]
     sample += sorted({ops.shape_of(o) for o in sg + sgf}, key=lambda s: s.flops())
     flops = secs = 0.0
     done = 0
@@ -104,9 +125,13 @@ def cpu_baseline(budget_s):
         done += 1
         if secs > budget_s:
             break
-    return {"value": round(flops / secs / 1e9, 3), "unit": "GFLOP/s", "cores": orc.num_threads(), "kind": "port",
-            "sample": "%d of %d ops: all 204 conv-ops-1-5-20 + sgemm-ops-small/full smallest first until the "
-                      "%.0f s budget, fp32, %.1f GFLOP in %.1f s" % (done, len(sample), budget_s, flops / 1e9, secs)}
+    line = {"value": round(flops / secs / 1e9, 3), "unit": "GFLOP/s", "cores": orc.num_threads(), "kind": "port",
+            "sample": "%d of %d ops: all 204 conv-ops-1-5-20 + 178 op_sigs_full ops, then sgemm-ops-small/full "
+                      "smallest first until the %.0f s budget; fp32 OpenMP (%d threads = OMP_NUM_THREADS, every "
+                      "thread the lease grants), %.1f GFLOP in %.1f s"
+                      % (done, len(sample), budget_s, orc.num_threads(), flops / 1e9, secs)}
+    line.update(cpu_info())
+    return line
 
 
 def main():
@@ -193,14 +218,18 @@ def main():
     # the same amortized back-to-back convention (src/culibs-wrap.cc:94-242 is the reference's seam).
     vtime = [None] * nop
     vinfo = [None] * nop
+    vendor_note = None
     if args.vendor == "on":
         from boda_hip import vendor
-        vd = vendor.Vendor(dd.local_rank % max(1, ndev))
-        for i in range(nop):
-            reps = max(3, min(50, int(round(2e-3 / max(ktime[i], 1e-6)))))
-            vinfo[i] = vd.time(my_shapes[i], reps)
-            vtime[i] = vinfo[i]["ms"] / 1e3
-        vd.close()
+        if not os.path.exists(vendor.LIB_PATH):  # comparator not built: the line says so
+            vendor_note = "libboda_hip_vendor.so not built: vendor_ms null"
+        else:
+            vd = vendor.Vendor(dd.local_rank % max(1, ndev))
+            for i in range(nop):
+                reps = max(3, min(50, int(round(2e-3 / max(ktime[i], 1e-6)))))
+                vinfo[i] = vd.time(my_shapes[i], reps)
+                vtime[i] = vinfo[i]["ms"] / 1e3
+            vd.close()
 
     my_flops = sum(s.flops() for s in my_shapes)
     total_flops = dd.sum(my_flops) * args.steps
@@ -278,6 +307,8 @@ def main():
         n_split = len({u[0] for u in units if u[1] != shapes[u[0]]})
         line = {
             "metric": "per-op GFLOPS and % fp32 roofline on sgemm-ops-full + conv-ops (AlexNet/NiN/GoogLeNet)",
+            "metric_note": "value aggregates the three lists of config.workload (the metric's two plus op_sigs_full, "
+                           "BASELINE config C5); per_set holds each list's own figures",
             "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": dd.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None,
@@ -290,6 +321,8 @@ def main():
                                      "HIP events on each op's first/last kernel dispatch (hipExtLaunchKernel), "
                                      "K extra eager steps after the timed region"),
                        "ops": len(shapes), "units": len(units), "ops_cut_into_panels": n_split,
+                       "panel_operands": "each column panel (M x n_j x K) owns contiguous a (K x M), b (K x n_j) "
+                                         "and c (M x n_j); no strided slice of a shared b",
                        "gflop_per_step": round(sum(s.flops() for s in shapes) / 1e9, 3),
                        "parallelism": "op-shard%d (LPT, no collective)" % dd.world,
                        "lpt_imbalance_predicted": round(pred_imb, 4),
@@ -298,7 +331,7 @@ def main():
                        "plat": dev.plat_tag(),
                        "vendor": ("rocblas_sgemm / MIOpen Find-chosen conv fwd + miopenOpTensor bias + "
                                   "miopenActivationForward ReLU, same units, amortized back-to-back calls, "
-                                  "context only" if args.vendor == "on" else None)},
+                                  "context only" if args.vendor == "on" and not vendor_note else vendor_note)},
             "per_set": per_set,
             "roofline": roof,
             "cpu_baseline": cpu,

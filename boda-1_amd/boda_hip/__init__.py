@@ -27,7 +27,7 @@ EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
            "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
-           "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
+           "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_dropout_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
            "bh_eltwise", "bh_conv2d_fwd_nchw_slab", "bh_conv2d_fwd_nchw_res", "bh_jit_build", "bh_jit_compile",
            "bh_jit_launch", "bh_jit_release"]
 
@@ -83,6 +83,7 @@ def lib():
         L.bh_pool_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 10 + [ctypes.c_int]
         L.bh_lrn_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 5 + [ctypes.c_float] * 3
         L.bh_relu_inplace.argtypes = [c_vp, c_vp, ctypes.c_uint64]
+        L.bh_dropout_inplace.argtypes = [c_vp, c_vp, ctypes.c_uint64, ctypes.c_float, c_u32]
         L.bh_softmax_chans.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 4
         L.bh_chan_copy.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 7
         L.bh_chan_affine.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 3 + [ctypes.c_int]
@@ -314,6 +315,9 @@ class Device:
 
     def relu(self, x, n):
         _check(lib().bh_relu_inplace(self.ctx, x.ptr, n))
+
+    def dropout(self, x, n, ratio, seed):
+        _check(lib().bh_dropout_inplace(self.ctx, x.ptr, n, ratio, seed))
 
     def softmax(self, inp, prob, B, C, H, W):
         _check(lib().bh_softmax_chans(self.ctx, inp.ptr, prob.ptr, B, C, H, W))

@@ -31,7 +31,7 @@ struct bh_ctx {
   uint64_t cnt_n = 0;
   void *wpack = nullptr;  // k-major filter bank for the ring conv kernels, grown on demand
   size_t wpack_bytes = 0;
-  // outgrown workspaces still referenced by captured graphs: freed with the context
+  // outgrown workspaces still referenced by captured graphs: freed with the last graph (or the context)
   // (a graph replays the pointers it was captured with)
   std::vector<void *> retired;
 };
@@ -48,7 +48,7 @@ int check_launch(const char *what);
 // first dispatch of the call records the start event and the last one the stop
 // event on the kernel's own dispatch (hipExtLaunchKernel).
 int launch(bh_ctx *ctx, const void *kernel, dim3 grid, dim3 block, void **args, bool first, bool last,
-           const char *what);
+           const char *what, uint32_t shmem = 0);
 
 // Magic-number unsigned division for 0 <= n < 2^31, 1 <= d < 2^31:
 // q = (umulhi(n, m) + n) >> s.
@@ -122,7 +122,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
                 float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                 uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0,
-                const float *res = nullptr, bool no_dc = false);
+                const float *res = nullptr, bool no_dc = false, bool repacked = false);
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX);
@@ -132,6 +132,7 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
 int launch_lrn(bh_ctx *ctx, const float *in, float *out, float *out_scale_base, uint32_t B, uint32_t C, uint32_t H,
                uint32_t W, uint32_t local_size, float alpha, float beta, float k);
 int launch_relu(bh_ctx *ctx, float *x, uint64_t n);
+int launch_dropout(bh_ctx *ctx, float *x, uint64_t n, float ratio, uint32_t seed);
 int launch_softmax(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W);
 int launch_chan_copy(bh_ctx *ctx, const float *in, float *out, uint32_t B, uint32_t HW, uint32_t in_c, uint32_t ic0,
                      uint32_t out_c, uint32_t oc0, uint32_t nc);

@@ -127,6 +127,22 @@ __global__ __launch_bounds__(256) void relu_kernel(float *__restrict__ x, uint64
   }
 }
 
+// Deterministic dropout in place (test/rtc/dropout.cucl, the rtc mode's Dropout with
+// has_conv_fwd_t::set_det_drop_seed): element i is kept, scaled by 1 / (1 - ratio), iff the
+// murmur3 finalizer of i + seed exceeds U32_MAX * ratio; else zeroed.
+__global__ __launch_bounds__(256) void dropout_kernel(float *__restrict__ x, uint32_t n, uint32_t thresh, float scale,
+                                                      uint32_t seed) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    uint32_t h = i + seed;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    x[i] = h > thresh ? x[i] * scale : 0.0f;
+  }
+}
+
 // Softmax over channels per pixel (test/rtc/softmax.cucl): max starts at 0 (as the reference),
 // exp(x - max), then divide by the sum.
 __global__ __launch_bounds__(256) void softmax_kernel(const float *__restrict__ in, float *__restrict__ prob,
@@ -259,6 +275,16 @@ int launch_relu(bh_ctx *ctx, float *x, uint64_t n) {
   if ((uintptr_t)x % 16) return fail(BH_UNSUP, "relu: pointer must be 16-byte aligned");
   void *args[] = {&x, &n};
   return launch(ctx, (const void *)relu_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), args, true, true, "relu");
+}
+
+int launch_dropout(bh_ctx *ctx, float *x, uint64_t n, float ratio, uint32_t seed) {
+  if (!(ratio > 0.0f && ratio < 1.0f)) return fail(BH_ERR, "dropout: ratio must be in (0, 1)");
+  if (n >= (1ull << 32)) return fail(BH_UNSUP, "dropout: tensor too large");
+  // the reference substitutes the ratio into its kernel text: double arithmetic on both
+  uint32_t n32 = (uint32_t)n, thresh = (uint32_t)(4294967295.0 * (double)ratio);
+  float scale = (float)(1.0 / (1.0 - (double)ratio));
+  void *args[] = {&x, &n32, &thresh, &scale, &seed};
+  return launch(ctx, (const void *)dropout_kernel, dim3(grid_for(n)), dim3(256), args, true, true, "dropout");
 }
 
 int launch_softmax(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W) {

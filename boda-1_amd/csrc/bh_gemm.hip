@@ -758,6 +758,7 @@ std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
     for (auto const &c : gv_cfgs()) v.push_back(c);
     for (auto const &c : dc_cfgs()) v.push_back(c);
     for (auto const &c : dcm_cfgs()) v.push_back(c);
+    for (auto const &c : k1s_cfgs()) v.push_back(c);
   }
   return v;
 }
@@ -1069,6 +1070,7 @@ std::string describe(int op, const uint32_t *d, choice_t const &ch) {
   }
   if (c.streamk) return s + "_streamk";
   if (c.dc == 2) return std::string("mfma32_conv_dm_") + c.name;
+  if (c.dc == 3) return std::string("mfma32_conv_k1s_") + c.name;
   if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
   if (c.fcv) return std::string("conv_fcv_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
@@ -1133,7 +1135,9 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases, float *out, uint32_t B,
                 uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
                 uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot, const float *res,
-                bool no_dc) {
+                bool no_dc, bool repacked) {
+  // repacked: a fallback call after this call's filter repack was already dispatched (that repack
+  // recorded the call's start event; no kernel of the fallback may record it again)
   // out_ctot: channels of the tensor `out` points into (0: OC). Every conv epilogue addresses
   // image i of the output at i * OCOHW, so a conv can write its channel slab of a wider
   // tensor (a Concat's output) in place.
@@ -1167,35 +1171,48 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
   if (no_dc && cfgs(1)[ch.cfg].dc) ch = heuristic(1, d, true, false);
+  const bool first = !repacked;
   if (cfgs(1)[ch.cfg].gv && !cfgs(1)[ch.cfg].packA) {
     // few output columns: stream the bank in its reference layout; the window covering the
-    // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads)
-    const bool fc = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0 && (uintptr_t)in % 16 == 0;
+    // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads). Shape
+    // mismatches are UNSUP; a shape the config serves with only a pointer misaligned for its
+    // vector loads falls back to the plain gv kernel (input) or the tile kernel (bank)
+    const bool fc_shape = OH == 1 && OW == 1 && KY == H && KX == W && py == 0 && px == 0;
+    const bool in16 = (uintptr_t)in % 16 == 0, fc = fc_shape && in16;
+    bool tile_fallback = !avec;
     if (cfgs(1)[ch.cfg].fcv) {
       // batch-streaming ipconv (bh_gv.hip fcv_kernel): a wave per BM / 4 bank rows
       const cfg_t &fc_c = cfgs(1)[ch.cfg];
-      if (!fc || !avec || B > (uint32_t)fc_c.BN)
+      if (!fc_shape || K % 4 || B > (uint32_t)fc_c.BN)
         return fail(BH_UNSUP, "conv: fcv configs need an ipconv (window = the whole unpadded input) at batch <= " +
                                   std::to_string(fc_c.BN) + " with K % 4 == 0");
-      void *args[] = {&p};
-      return bh::launch(ctx, (const void *)fc_c.k[A_MVEC][B_FC][0], dim3((OC + fc_c.BM - 1) / fc_c.BM), dim3(256), args,
-                        true, true, "conv");
-    }
-    if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
+      if (fc && avec) {
+        void *args[] = {&p};
+        return bh::launch(ctx, (const void *)fc_c.k[A_MVEC][B_FC][0], dim3((OC + fc_c.BM - 1) / fc_c.BM), dim3(256),
+                          args, first, true, "conv");
+      }
+      tile_fallback = true;  // 16-B loads of the bank or the input rows impossible
+    } else if (cfgs(1)[ch.cfg].k[A_MVEC][B_IM1X1S][0]) {
       // gvo (bh_gv.hip): 1x1 over the reference-layout bank, 16-deep k groups; an ipconv takes
       // its input rows as the columns (B_FC, one 16-B load per column tile and k group)
-      if (fc && K % 16 == 0 && avec && cfgs(1)[ch.cfg].k[A_MVEC][B_FC][0])
-        return launch_gemm(ctx, 1, ch, A_MVEC, B_FC, p, "conv");
-      if (!k1 || IC % 16 || !avec) return fail(BH_UNSUP, "conv: gvo configs need a 1x1 conv with IC % 16 == 0");
-      if ((OH * OW) % (uint32_t)cfgs(1)[ch.cfg].gv_cx)
-        return fail(BH_UNSUP, "conv: interleaved-column configs need OH*OW % run == 0");
-      return launch_gemm(ctx, 1, ch, A_MVEC, B_IM1X1S, p, "conv");
+      const int cx = cfgs(1)[ch.cfg].gv_cx;
+      if (fc_shape && K % 16 == 0 && cfgs(1)[ch.cfg].k[A_MVEC][B_FC][0]) {
+        if (fc && avec) return launch_gemm(ctx, 1, ch, A_MVEC, B_FC, p, "conv", first);
+        tile_fallback = true;
+      } else {
+        if (!k1 || IC % 16) return fail(BH_UNSUP, "conv: gvo configs need a 1x1 conv with IC % 16 == 0");
+        if ((OH * OW) % (uint32_t)cx) return fail(BH_UNSUP, "conv: interleaved-column configs need OH*OW % run == 0");
+        if (avec && (uintptr_t)in % (4u * cx) == 0) return launch_gemm(ctx, 1, ch, A_MVEC, B_IM1X1S, p, "conv", first);
+        tile_fallback = true;  // 16-B bank rows or CX-wide pixel runs of the input misaligned
+      }
+    } else if (avec) {
+      return launch_gemm(ctx, 1, ch, A_MVEC, fc ? B_FC : (k1 ? B_IM1X1 : B_IM2COL), p, "conv", first);
     }
-    if (avec)
-      return launch_gemm(ctx, 1, ch, A_MVEC, fc ? B_FC : (k1 ? B_IM1X1 : B_IM2COL), p, "conv");
-    ch = choice_t{};  // unaligned bank (K % 4 or pointer): a tile kernel
-    ch.cfg = cfg_index(1, "128x32x32");
-    ch.red = 1;
+    if (tile_fallback) {
+      ch = choice_t{};  // unaligned bank (K % 4 or pointer) or input: a tile kernel
+      ch.cfg = cfg_index(1, "128x32x32");
+      ch.red = 1;
+    }
   }
   if (cfgs(1)[ch.cfg].packA) {
     // ring kernels read the filter bank k-major: repack it first (this call's first dispatch)
@@ -1206,12 +1223,15 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
     if (pk_floats * 4 >= 0x7fffffc0ull || in_bytes >= (1ull << 30)) {
       ch = heuristic(1, d, false);
     } else {
+      bool rp = repacked;  // a repack of this call already dispatched (it recorded the start event)
       if (!wp) {
         int rc = ensure_wpack(ctx, pk_floats * 4);
-        if (rc == BH_OK) rc = launch_xpose_filts(ctx, filts, (float *)ctx->wpack, OC, IC, KY * KX, true, false);
+        if (rc == BH_OK) rc = launch_xpose_filts(ctx, filts, (float *)ctx->wpack, OC, IC, KY * KX, first, false);
         if (rc != BH_OK) return rc;
         wp = (const float *)ctx->wpack;
+        rp = true;
       }
+      const bool kfirst = !rp;  // the main kernel is the call's first dispatch
       p.a = wp;
       p.lda = oc4;
       p.a_bytes = kp * oc4 * 4;
@@ -1219,11 +1239,12 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       set_fd(IC, p.ic_m, p.ic_s);
       if (cfgs(1)[ch.cfg].dc) {
         const cfg_t &dcc = cfgs(1)[ch.cfg];
-        const int rc = dcc.dc == 2 ? launch_dcm(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, packed != nullptr)
-                                   : launch_dc(ctx, dcc, p, B, KY, KX, sy, sx, packed != nullptr);
+        const int rc = dcc.dc == 2   ? launch_dcm(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, kfirst)
+                       : dcc.dc == 3 ? launch_k1s(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, kfirst)
+                                     : launch_dc(ctx, dcc, p, B, KY, KX, sy, sx, kfirst);
         if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
-        return launch_conv(ctx, in, filts, packed ? packed : wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py,
-                           px, relu, out_ctot, res, true);
+        return launch_conv(ctx, in, filts, wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, out_ctot,
+                           res, true, rp);
       }
       if (cfgs(1)[ch.cfg].gv) {
         // register streaming over the packed bank (bh_gv.hip gvp_kernel): 16-deep k groups
@@ -1231,16 +1252,17 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
         if (IC % 16) return fail(BH_UNSUP, "conv: gvp configs need IC % 16 == 0");
         if (cfgs(1)[ch.cfg].gv_cx > 1 && (!k1 || (OH * OW) % (uint32_t)cfgs(1)[ch.cfg].gv_cx))
           return fail(BH_UNSUP, "conv: interleaved-column configs need a 1x1 conv with OH*OW % run == 0");
-        return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1S : B_IMTAP, p, "conv", packed != nullptr);
+        return launch_gemm(ctx, 1, ch, A_KVEC, k1 ? B_IM1X1S : B_IMTAP, p, "conv", kfirst);
       }
       const uint32_t bk = (uint32_t)cfgs(1)[ch.cfg].BK;
       const bool tab = ((p.K + bk - 1) / bk) * bk <= (uint32_t)TAB_MAX;  // K rows a block tabulates
       const int bld = k1 ? (IC % bk == 0 ? B_IM1X1S : B_IM1X1)
                          : (IC >= bk ? (IC % bk == 0 ? B_IMTAP : B_IMT2) : (tab ? B_IMTAB : B_IM2COL));
-      return launch_gemm(ctx, 1, ch, A_KVEC, bld, p, "conv", packed != nullptr);
+      return launch_gemm(ctx, 1, ch, A_KVEC, bld, p, "conv", kfirst);
     }
   }
-  return launch_gemm(ctx, 1, ch, avec ? A_MVEC : A_MSCALAR, k1v ? B_IM1X1V : (k1 ? B_IM1X1 : B_IM2COL), p, "conv");
+  return launch_gemm(ctx, 1, ch, avec ? A_MVEC : A_MSCALAR, k1v ? B_IM1X1V : (k1 ? B_IM1X1 : B_IM2COL), p, "conv",
+                     first);
 }
 
 }  // namespace bh

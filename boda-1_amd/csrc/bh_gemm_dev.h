@@ -330,7 +330,7 @@ struct cfg_t {
   int streamk = 0;    // persistent stream-K grid (srk_kernel): k[..][..][0] only
   int lds_bytes = 0;  // static LDS per block (stream-K grid sizing)
   int gv = 0;         // filter-streaming kernel (bh_gv.hip): grid (M / BM) x K chunks, BN >= N
-  int dc = 0;         // direct conv (bh_direct.hip): kernel dc_ky x dc_kx, stride dc_s, strip dc_rin x dc_wpm
+  int dc = 0;         // direct conv (bh_direct.hip; 2: bh_dcm.hip, 3: bh_k1s.hip): kernel dc_ky x dc_kx, stride dc_s, strip dc_rin x dc_wpm
   int dc_ky = 0, dc_kx = 0, dc_s = 0, dc_wpm = 0, dc_rin = 0;
   int dc_ci = 0;      // dc == 2 (bh_dcm.hip): input channels per stage
   int gv_cx = 1;      // gv: interleaved column tiles (1x1, a lane's gv_cx pixels per load)
@@ -349,6 +349,10 @@ int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY,
 // bh_dcm.hip: multi-channel direct-conv configurations for stride-1 3x3 / 5x5 convs
 std::vector<cfg_t> dcm_cfgs();
 int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+               uint32_t sx, uint32_t splits, bool first);
+// bh_k1s.hip: 1x1 convs with the bank slice resident in LDS, input streamed into registers
+std::vector<cfg_t> k1s_cfgs();
+int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
                uint32_t sx, uint32_t splits, bool first);
 // split-K / stream-K workspace and arrival tickets of the context (bh_gemm.hip)
 int ensure_ws(bh_ctx *ctx, size_t bytes);

@@ -112,18 +112,16 @@ int bh_jit_launch(bh_ctx *c, int module_id, const char *name, void **args, uint3
   if (!name) return bh::fail(BH_ERR, "null function name");
   if (!blks || !tpb) return bh::fail(BH_ERR, std::string("jit launch of '") + name + "' with zero blks or tpb");
   if ((uint64_t)blks * tpb > 0xffffffffull) return bh::fail(BH_UNSUP, "jit launch: grid too large");
-  hipFunction_t f = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_jit_mu);
-    auto it = g_modules.find({c, module_id});
-    if (it == g_modules.end()) return bh::fail(BH_ERR, "jit launch: unknown module");
-    auto fit = it->second.funcs.find(name);
-    if (fit == it->second.funcs.end())
-      return bh::fail(BH_ERR, std::string("jit launch: '") + name + "' is not a function of the module");
-    f = fit->second;
-  }
+  // the lock is held until the launch is enqueued: a concurrent bh_jit_release then unloads the
+  // module only after its stream has run this launch (it synchronises the stream after erasing)
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  auto it = g_modules.find({c, module_id});
+  if (it == g_modules.end()) return bh::fail(BH_ERR, "jit launch: unknown module");
+  auto fit = it->second.funcs.find(name);
+  if (fit == it->second.funcs.end())
+    return bh::fail(BH_ERR, std::string("jit launch: '") + name + "' is not a function of the module");
   // global size in work-items (hipExtModuleLaunchKernel takes the grid in threads)
-  BH_HIP(hipExtModuleLaunchKernel(f, blks * tpb, 1, 1, tpb, 1, 1, 0, c->stream, args, nullptr, c->t_start,
+  BH_HIP(hipExtModuleLaunchKernel(fit->second, blks * tpb, 1, 1, tpb, 1, 1, 0, c->stream, args, nullptr, c->t_start,
                                   c->t_stop, 0));
   return BH_OK;
 }

@@ -1,0 +1,337 @@
+// bh_k1s.hip -- 1x1 convolutions over many pixels with the filter bank resident in LDS and the
+// input streamed straight into registers (Boda's k1conv role: test/rtc/k1conv.cucl, chosen at
+// src/cnn_op.cc:51-58).
+//
+// A 1x1 conv is one GEMM per image, out[oc][p] = bias[oc] + sum_ic W[oc][ic] in[ic][p], with
+// few channels (K = IC <= a few hundred) and many pixels: the op streams the input and output
+// (HBM) and its MFMA work is of the same order, so nothing may stand between the two streams.
+// The tile kernels re-fetch the bank per pixel tile, split K, stage the input through LDS and
+// synchronise their waves at every stage (bh_dcm.hip's 1x1 mode: 0.32-0.36 of roofline on the
+// conv set's batch-20 1x1 ops). Here:
+//  * a block owns one OC tile of OCT = 32*TM output channels for its whole life: its slice of
+//    the k-major packed bank (bh_conv_filts_pack, [K][OC4]), rows [IC][OCT], is DMA'd into LDS
+//    once (16-B pieces, chunk by chunk along with the first unit's input, a barrier per chunk
+//    in that unit only); lane li computes channels li + 32 t: one ds_read_b32 per tile and step;
+//  * a wave owns a unit of 32 consecutive pixels of the flattened (image, pixel) space x the
+//    block's OCT channels x the whole K: v_mfma_f32_32x32x2_f32 with A = the input (lane li's
+//    pixel, channel 2s + lane/32: one dword load per lane per k step, 2 x 128 contiguous bytes
+//    per wave instruction, straight into the operand register), B = the resident bank;
+//  * the loads run Q-1 chunks of KC channels ahead through a register ring (vmcnt-counted, no
+//    drains), across unit boundaries: a wave never waits for its next unit's first loads; the
+//    waves of a block never synchronise after the prologue (no barrier, no split-K, no slabs);
+//  * the epilogue stores float4 pixel quads (bias, residual, ReLU) straight from the
+//    accumulators: lane (li, h) holds channel li + 32 t, pixels 8g + 4h .. + 3 of its unit.
+// Blocks b, b + 8, ... share an XCD under round-robin placement; the blocks of one XCD cover all
+// OC tiles of the same pixel units, so an input unit read by several OC tiles is re-read from
+// that XCD's L2.
+// Same GemmArgs contract as the other conv kernels: a = packed bank, lda = OC4, b = input,
+// OCOHW = the output's image stride (channel-slab outputs work), tiles_m = OC tiles.
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+namespace {
+
+// DBG (diagnostic builds in the instrumented library only; wrong results by design): bit 0 = no
+// input loads after the prologue, bit 1 = no MFMA, bit 2 = no output stores (dropped instead)
+template <int TM, int KC, int Q, int NW, int DBG = 0>
+__global__ __launch_bounds__(NW * 64) void k1s_kernel(GemmArgs p) {
+  constexpr int OCT = 32 * TM;           // output channels of the block (LDS floats per bank row)
+  constexpr int SC = KC / 2;             // k steps (and input loads per lane) per chunk
+  constexpr int S = 4 * TM;              // float4 stores per lane per unit
+  constexpr int PF = 3;                  // LDS fragment prefetch (steps)
+  constexpr int WPC = KC * OCT / 4;      // 16-B bank pieces per chunk
+  constexpr int LWC = (WPC + NW * 64 - 1) / (NW * 64);  // bank DMA instructions per lane per chunk
+  static_assert(TM >= 1 && TM <= 4 && KC % 2 == 0, "tile");
+  static_assert(Q >= 2 && (Q - 1) * SC + S <= 63, "vmcnt range");
+  static_assert(SC % (PF + 1) == 0, "fragment ring period divides a chunk");
+  constexpr int SP = 36;                 // staging tile pitch (floats): 32 pixels + 4
+  // the bank slice [IC][OCT] (packed-bank rows oc0 ..), then each wave's epilogue tile [32][SP]
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  KT(0);
+  // block -> (OC tile, index among the blocks of that tile); tiles_m = OC tiles, gridDim.x a
+  // multiple of 8 * tiles_m
+  const uint32_t l8 = blockIdx.x >> 3;
+  const uint32_t oct = l8 % p.tiles_m;
+  const uint32_t gi = (l8 / p.tiles_m) * 8 + (blockIdx.x & 7);
+  const uint32_t wg = (gridDim.x / p.tiles_m) * NW;  // waves per OC tile
+  const uint32_t oc0 = oct * OCT;
+  const uint32_t npu = (p.N + 31) / 32, nch = p.K / KC;
+  const uint32_t lds_w = p.K * OCT;  // floats of the bank slice
+  const uint32_t hw4 = p.HW * 4u;
+
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsx = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+
+  // lane (li, kh) computes output channels oc0 + li + 32 t (t < TM): B fragment of tile t at
+  // step s is bank row 2s + kh, column li + 32 t -- one ds_read_b32 per tile and step
+  float bias[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const uint32_t oc = oc0 + li + 32 * t;
+    bias[t] = ld1(rsbias, oob_unless(oc < p.M, oc * 4u));
+  }
+  // the bank slice [IC][OCT] comes in with the first unit's chunks: 16-B pieces of packed-bank
+  // row k, columns oc0 + 4 q .. (OC4-padded rows: columns past OC4 miss); piece e of a chunk
+  // (lanes past the chunk's pieces write nothing: the next chunk's rows may already have landed.
+  // No wait ever counts on these DMAs -- they only add younger operations -- so a wave that
+  // issues fewer of them keeps every wait correct)
+  uint32_t wsrc[LWC];
+#pragma unroll
+  for (int j = 0; j < LWC; ++j) {
+    const uint32_t e = (uint32_t)((j * NW + wave) * 64 + lane), r = e / (OCT / 4), q = e % (OCT / 4);
+    wsrc[j] = e < (uint32_t)WPC ? oob_unless(oc0 + 4 * q < p.lda, (r * p.lda + oc0 + 4 * q) * 4u) : 0xffffffffu;
+  }
+  auto issue_w = [&](uint32_t c) {  // chunk c's bank rows (the whole K of them stays resident)
+#pragma unroll
+    for (int j = 0; j < LWC; ++j)
+      if (wsrc[j] != 0xffffffffu)
+        dma16s(rsw, wl + (size_t)c * KC * OCT + (j * NW + wave) * 256, wsrc[j], c * KC * p.lda * 4u);
+  };
+  // per-lane input offset of unit pu (pixel pu*32 + li, channel kh); past the op: misses
+  auto ubase = [&](uint32_t pu) -> uint32_t {
+    const uint32_t n = pu * 32 + li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    return oob_unless((pu < npu) & (n < p.N), (img * p.ICHW + pix + kh * p.HW) * 4u);
+  };
+  float xr[Q][SC];
+  // chunk c of a unit: the chunk offset goes into the lane's VGPR offset (a miss stays a miss:
+  // OOB + c * KC * HW * 4 < 2^32), step s's channel pair into the scalar soffset (SC values shared
+  // by every chunk: few SGPRs)
+  auto issue = [&](int q, uint32_t base, uint32_t c) {
+    const uint32_t vb = (DBG & 1) ? OOB : base + c * KC * hw4;
+#pragma unroll
+    for (int s = 0; s < SC; ++s)
+      xr[q][s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsx, vb, 2 * s * hw4, 0));
+  };
+  uint32_t pu = gi * NW + wave;
+  uint32_t bcur = ubase(pu), bnext = ubase(pu + wg);
+#pragma unroll
+  for (int q = 0; q < Q - 1; ++q) {
+    issue_w(q);
+    issue(q, bcur, q);
+  }
+  // S dropped stores: the loop's waits count a unit's epilogue stores behind the first chunks
+  // of the next unit, and the first unit has the same VMEM sequence (its bank DMAs only add
+  // younger operations: those waits are stricter than needed)
+#pragma unroll
+  for (int s = 0; s < S; ++s) __builtin_amdgcn_raw_buffer_store_b32(0u, rso, OOB, 0, 0);
+
+  f32x16 acc[TM];
+  float wf[PF + 1][TM];
+  const float *const wb = wl + kh * OCT + li;  // bank row kh, column li, this lane
+  auto frag = [&](float (&w)[TM], uint32_t c, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) w[t] = wb[(c * KC + 2 * s) * OCT + 32 * t];
+  };
+
+  // chunk c = cq + r (slot r % Q) of the current unit: wait for its loads (first unit: and for
+  // every wave's bank DMA of the chunk), put chunk c + Q - 1 (of this unit or the next) in flight,
+  // MFMAs with the fragments PF steps ahead (the first unit reads the next chunk's fragments only
+  // after the next barrier)
+  auto chunk = [&](int r, uint32_t cq, bool first, bool u0) {
+    if (first && r < Q - 1) vm_wait<(Q - 2) * SC + S>();
+    else vm_wait<(Q - 2) * SC>();
+    if (u0) {
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < PF; ++s) frag(wf[s], cq + r, s);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const uint32_t c2 = cq + (uint32_t)(r + Q - 1);
+      const bool nx = c2 >= nch;
+      if (u0 && !nx) issue_w(c2);
+      issue((r + Q - 1) % Q, nx ? bnext : bcur, nx ? c2 - nch : c2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t c = cq + (uint32_t)r, cn = c + 1 == nch ? 0u : c + 1;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {
+      if (s + PF < SC) frag(wf[(s + PF) % (PF + 1)], c, s + PF);
+      else if (!u0) frag(wf[(s + PF) % (PF + 1)], cn, s + PF - SC);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        if constexpr ((DBG & 2) != 0) acc[t][s] += xr[r % Q][s] * wf[s % (PF + 1)][t];
+        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[r % Q][s], wf[s % (PF + 1)][t], acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const bool vec_ok = !p.res;
+  // unit loop; the first pass runs in every wave (a wave without a unit computes on misses and
+  // stores nothing) so that all waves meet the first unit's per-chunk barriers
+  for (bool u0 = true;; u0 = false) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    if (u0) {
+#pragma unroll
+      for (int r = 0; r < Q; ++r) chunk(r, 0, true, true);
+      for (uint32_t cq = Q; cq < nch; cq += Q) {
+#pragma unroll
+        for (int r = 0; r < Q; ++r) chunk(r, cq, false, true);
+      }
+      // the whole bank is resident from here on: fragments of the next unit's first steps
+#pragma unroll
+      for (int s = 0; s < PF; ++s) frag(wf[s], 0, s);
+    } else {
+#pragma unroll
+      for (int r = 0; r < Q; ++r) chunk(r, 0, true, false);
+      for (uint32_t cq = Q; cq < nch; cq += Q) {
+#pragma unroll
+        for (int r = 0; r < Q; ++r) chunk(r, cq, false, false);
+      }
+    }
+#ifdef BH_KTRACE
+    if (u0) KT(2);
+#endif
+    // epilogue, staged per OC tile through the wave's own LDS tile [32 oc][32 px] (no barrier):
+    // lane (li, kh) holds channel oc0 + li + 32 t, pixels pu*32 + 8g + 4kh + e; read back, lane L
+    // holds channel row 8j + L/8 of the tile, pixels 4 (L % 8) .. + 3, so a store instruction
+    // writes 8 output rows x 128 contiguous bytes (not 32 rows x 32 B: 4x the line fragments)
+    {
+      const uint32_t q4 = 4u * (uint32_t)(lane & 7), rr = (uint32_t)(lane >> 3);
+      const uint32_t n = pu * 32 + q4;  // this lane's first pixel after the transpose
+      const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+      const bool quad = vec_ok & (pix + 4 <= p.OHW) & (n < p.N) & (pu < npu);
+      const uint32_t obase = img * p.OCOHW + pix;
+      float *const st = wl + lds_w + wave * (32 * SP);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4v v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
+          *(f32x4v *)(st + li * SP + 8 * g + 4 * kh) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t r = 8u * j + rr, oc = oc0 + 32u * t + r;
+          f32x4v v = *(const f32x4v *)(st + r * SP + q4);
+          const float bb = __shfl(bias[t], (int)r);  // bias of channel row r (held by lane r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bb;
+          const uint32_t o = oob_unless((oc < p.M) & (pu < npu), (obase + oc * p.OHW) * 4u);
+          f32x4v y = v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[e] = (p.relu && y[e] < 0.0f) ? 0.0f : y[e];
+          // always issued (dropped where the quad goes element by element): every unit has at
+          // least S vector stores, which the loop's waits count on
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y),
+                                                 rso, quad && (DBG & 4) == 0 ? o : OOB, 0, AUX_OUT);
+          if (!quad && (oc < p.M) && (pu < npu)) {
+            // a quad past its image or the op, or a residual epilogue: element by element (more
+            // VMEM instructions than counted only make the waits stricter)
+            const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t ne = n + e;
+              const uint32_t ie = fdiv(ne, p.ohw_m, p.ohw_s);
+              const uint32_t oe = oob_unless(ne < p.N, (ie * p.OCOHW + oc * p.OHW + ne - ie * p.OHW) * 4u);
+              float z = v[e];
+              if (p.res) z += ld1(rsr, oe);
+              z = (p.relu && z < 0.0f) ? 0.0f : z;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, oe, 0, AUX_OUT);
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+      }
+    }
+#ifdef BH_KTRACE
+    if (u0) KT(3);
+#endif
+    pu += wg;
+    if (pu >= npu) break;
+    bcur = bnext;
+    bnext = ubase(pu + wg);
+  }
+  vm_wait<0>();
+  KT(4);
+}
+
+template <int TM, int KC, int Q, int NW, int DBG = 0>
+cfg_t k1s_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * NW, KC, 64 * NW, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = k1s_kernel<TM, KC, Q, NW, DBG>;
+  c.dc = 3;
+  c.dc_ky = 1;
+  c.dc_kx = 1;
+  c.dc_ci = KC;
+  c.dc_rin = Q;
+  return c;
+}
+
+}  // namespace
+
+std::vector<cfg_t> k1s_cfgs() {
+  // <TM, KC, Q, NW>: OC tile 32*TM, KC-channel chunks, Q - 1 chunks in flight, NW waves
+  return {
+      k1s_cfg<1, 32, 3, 4>("ks32c32q3"),    k1s_cfg<2, 32, 3, 4>("ks64c32q3"),
+      k1s_cfg<3, 32, 3, 4>("ks96c32q3"),    k1s_cfg<4, 32, 3, 4>("ks128c32q3"),
+      k1s_cfg<1, 32, 4, 4>("ks32c32q4"),    k1s_cfg<2, 32, 4, 4>("ks64c32q4"),
+      k1s_cfg<2, 32, 2, 4>("ks64c32q2"),    k1s_cfg<4, 32, 2, 4>("ks128c32q2"),
+      k1s_cfg<2, 16, 4, 4>("ks64c16q4"),    k1s_cfg<3, 16, 4, 4>("ks96c16q4"),
+      k1s_cfg<4, 16, 4, 4>("ks128c16q4"),   k1s_cfg<1, 16, 4, 4>("ks32c16q4"),
+      k1s_cfg<2, 32, 3, 8>("ks64c32q3w8"),  k1s_cfg<3, 32, 3, 8>("ks96c32q3w8"),
+      k1s_cfg<1, 32, 3, 8>("ks32c32q3w8"),  k1s_cfg<1, 16, 4, 8>("ks32c16q4w8"),
+#ifdef BH_KTRACE
+      k1s_cfg<3, 32, 3, 4, 1>("xks96c32q3_noload"), k1s_cfg<3, 32, 3, 4, 2>("xks96c32q3_nomfma"),
+      k1s_cfg<3, 32, 3, 4, 4>("xks96c32q3_nostore"), k1s_cfg<3, 32, 3, 4, 7>("xks96c32q3_none"),
+#endif
+  };
+}
+
+// Launch a resident-bank 1x1 configuration (p filled by launch_conv with a = packed bank): UNSUP
+// unless the shape is a stride-1 unpadded 1x1 conv whose K is a whole number of trips (Q chunks
+// of KC channels) and whose bank slice fits the LDS. splits: 0 = two blocks per CU where they
+// fit, 1..4 = blocks per CU.
+int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
+               uint32_t sx, uint32_t splits, bool first) {
+  (void)B;
+  if (KY != 1 || KX != 1 || sy != 1 || sx != 1 || p.py || p.px)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for unpadded stride-1 1x1 convs");
+  const uint32_t KC = (uint32_t)c.dc_ci, Q = (uint32_t)c.dc_rin, NT = (uint32_t)c.NT;
+  if (p.K % KC || (p.K / KC) % Q)
+    return bh::fail(BH_UNSUP, std::string("conv: input channels not a whole number of ") + c.name + " trips");
+  // the bank slice [IC][OCT] and one [32][36] epilogue staging tile per wave
+  const uint64_t lds = ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;
+  if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: bank slice too large for ") + c.name);
+  const uint64_t out_bytes = (uint64_t)p.OCOHW * (p.N / p.OHW) * 4;
+  if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the k1s kernel");
+  p.c_bytes = (uint32_t)out_bytes;
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return bh::fail(BH_ERR, "conv: k1s LDS attribute");
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, c.NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+  const uint32_t oct = (p.M + c.BM - 1) / c.BM;
+  const uint32_t npu = (p.N + 31) / 32, nw = NT / 64;
+  uint32_t bpc = splits ? splits : 2;
+  bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  // blocks per OC tile: enough waves for every pixel unit, at most the CUs' share; a multiple of 8
+  uint64_t per = std::max<uint64_t>(1, ((uint64_t)ncu * bpc) / oct);
+  per = std::min<uint64_t>(per, (npu + nw - 1) / nw);
+  per = (per + 7) / 8 * 8;
+  const uint64_t G = per * oct;
+  if (G >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: k1s grid too large");
+  p.tiles_m = oct;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(c.NT), args, first, true, "conv_k1s", (uint32_t)lds);
+}
+
+}  // namespace bhk

@@ -66,10 +66,10 @@ int grow_buffer(bh_ctx *ctx, void *&buf, size_t &have, size_t want, bool zero, c
 }
 
 int launch(bh_ctx *ctx, const void *kernel, dim3 grid, dim3 block, void **args, bool first, bool last,
-           const char *what) {
+           const char *what, uint32_t shmem) {
   hipEvent_t b = first ? ctx->t_start : nullptr, e = last ? ctx->t_stop : nullptr;
-  hipError_t r = (b || e) ? hipExtLaunchKernel(kernel, grid, block, args, 0, ctx->stream, b, e, 0)
-                          : hipLaunchKernel(kernel, grid, block, args, 0, ctx->stream);
+  hipError_t r = (b || e) ? hipExtLaunchKernel(kernel, grid, block, args, shmem, ctx->stream, b, e, 0)
+                          : hipLaunchKernel(kernel, grid, block, args, shmem, ctx->stream);
   if (first) ctx->t_start = nullptr;
   if (last) ctx->t_stop = nullptr;
   if (r != hipSuccess) return fail(BH_ERR, std::string("launch of ") + what + " failed: " + hipGetErrorString(r));
@@ -338,6 +338,13 @@ int bh_relu_inplace(bh_ctx *c, float *x, uint64_t n) {
   return bh::launch_relu(c, x, n);
 }
 
+int bh_dropout_inplace(bh_ctx *c, float *x, uint64_t n, float ratio, uint32_t det_drop_seed) {
+  BH_ENTER_CALL(c);
+  if (!x) return bh::fail(BH_ERR, "null tensor");
+  if (!n) return BH_OK;
+  return bh::launch_dropout(c, x, n, ratio, det_drop_seed);
+}
+
 int bh_softmax_chans(bh_ctx *c, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W) {
   BH_ENTER_CALL(c);
   if (!in || !prob) return bh::fail(BH_ERR, "null tensor");
@@ -450,6 +457,13 @@ int bh_graph_destroy(bh_ctx *c, int graph_id) {
   BH_HIP(hipStreamSynchronize(c->stream));
   BH_HIP(hipGraphExecDestroy(c->graphs[graph_id]));
   c->graphs[graph_id] = nullptr;
+  // outgrown workspaces were kept for the graphs that captured them: free them with the last one
+  bool live_graph = false;
+  for (hipGraphExec_t g : c->graphs) live_graph |= g != nullptr;
+  if (!live_graph) {
+    for (void *r : c->retired) BH_HIP(hipFree(r));
+    c->retired.clear();
+  }
   return BH_OK;
 }
 

@@ -177,7 +177,8 @@ dims_t nchw(uint32_t b, uint32_t c, uint32_t y, uint32_t x) {
 }
 }  // namespace
 
-p_conv_pipe_t create_pipe_from_prototxt(std::string const &text, uint32_t img, std::string const &out_node) {
+p_conv_pipe_t create_pipe_from_prototxt(std::string const &text, uint32_t img, std::string const &out_node,
+                                        bool det_dropout) {
   p_pt_msg net = parse_prototxt(text);
   auto cp = std::make_shared<conv_pipe_t>();
   cp->name = net->get("name", "net");
@@ -251,9 +252,12 @@ p_conv_pipe_t create_pipe_from_prototxt(std::string const &text, uint32_t img, s
       p_pt_msg p = lp->sub("scale_param");
       op->bias_term = p && p->get("bias_term", "false") == "true";
     } else if (op->type == "Dropout") {
-      // the forward (TEST) net: identity; in place -> no op, else a copy
-      if (op->tops == op->bots) { keep = false; why = "Dropout in place (identity at test time)"; }
-      else op->type = "Copy";
+      // the forward (TEST) net: identity; in place -> no op, else a copy. det_dropout: the rtc
+      // mode's deterministic mask (an in-place op, src/rtc_fwd.cc:348-358)
+      p_pt_msg p = lp->sub("dropout_param");
+      op->dropout_ratio = p ? f32(p->get("dropout_ratio", "0.5"), "dropout_ratio") : 0.5f;
+      if (op->tops != op->bots) op->type = "Copy";
+      else if (!det_dropout) { keep = false; why = "Dropout in place (identity at test time)"; }
     } else if (op->type == "Data") {
       p_pt_msg tp = lp->sub("transform_param"), dp = lp->sub("data_param");
       if (!tp || !dp) rt_err("Data layer '" + op->tag + "' without transform_param / data_param");
@@ -579,7 +583,7 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     std::vector<float> w((size_t)s.OC * s.IC * s.KY * s.KX);
     synth_param(w, param_seed(op.tag, "filts"), std::sqrt(3.0f / (float)(s.IC * s.KY * s.KX)) / 5.0f);
     std::vector<float> b(s.OC, 0.0f);
-    if (op.bias_term) synth_param(b, param_seed(op.tag, "biases"), 0.1f / 5.0f);
+    if (op.bias_term && !force_zero_bias) synth_param(b, param_seed(op.tag, "biases"), 0.1f / 5.0f);
     auto fit = folds.find(op.tag);
     const bool fold = fit != folds.end();
     if (fold) {
@@ -641,6 +645,15 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     }
     rtc->compile({{"hip_relu__" + op.tag, "", {}, fo}}, rtc_compile_opts_t());
     add_call("hip_relu__" + op.tag, op, {{"x", op.tops[0]}});
+    return;
+  }
+  if (op.type == "Dropout") {  // in place; the seed is a call argument (set_det_drop_seed)
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%.9g", op.dropout_ratio);
+    fo.str_vals = {{"dropout_ratio", buf}};
+    rtc->compile({{"hip_dropout__" + op.tag, "", {}, fo}}, rtc_compile_opts_t());
+    add_call("hip_dropout__" + op.tag, op, {{"inout", op.tops[0]}, {"det_drop_seed", rtc_arg_t::u32(det_drop_seed)}});
+    dropout_cixs.push_back((uint32_t)calls.size() - 1);
     return;
   }
   if (op.type == "Pooling") {
@@ -718,7 +731,7 @@ void conv_pipe_fwd_t::upload(std::string const &vn, std::vector<float> const &v)
   rtc->copy_nda_to_var(vn, n);
 }
 
-void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, p_rtc_compute_t const &rtc_) {
+void conv_pipe_fwd_t::init_with_rtc(p_conv_pipe_t const &cp_, p_rtc_compute_t const &rtc_) {
   cp = cp_;
   rtc = rtc_;
   for (auto const &in : cp->inputs) {
@@ -732,21 +745,163 @@ void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, p_rtc_compute_t const &rtc_
   rtc->finish_and_sync();
 }
 
-void conv_pipe_fwd_t::run_fwd(std::map<std::string, p_nda_t> const &inputs) {
-  for (auto const &kv : inputs) rtc->copy_nda_to_var(kv.first, kv.second);
+// src/rtc_fwd.cc:469-533: the mode's options from nia, the backend (NESI "rtc", default be=hip
+// on device 0; Boda picks nvrtc / ocl by enabled feature), then the executor
+void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, nesi_init_arg_t *const nia) {
+  if (!cp_) rt_err("conv_pipe_fwd_t::init: null conv_pipe");
+  nesi_init_arg_t none;
+  nesi_init_arg_t &a = nia ? *nia : none;
+  enable_prof = a.get_u32("enable_prof", 1);
+  enable_double_run = a.get_u32("enable_double_run", 0);
+  enable_stats = a.get_u32("enable_stats", 0);
+  force_zero_bias = a.get_u32("force_zero_bias", 0);
+  per_call_fn = a.get_str("per_call_fn", "");
+  graph_reps = a.get_u32("graph_reps", 0);
+  pack_filts = a.get_bool("pack_filts", true);
+  fold_affines = a.get_bool("fold_affines", true);
+  concat_in_place = a.get_bool("concat_in_place", true);
+  fuse_residual = a.get_bool("fuse_residual", true);
+  dump_vars.clear();
+  if (a.has("dump_vars")) {  // "(0=blob,1=blob,...)" or "blob:blob"
+    p_lexp_t l = a.nvm.at("dump_vars");
+    a.used.insert("dump_vars");
+    if (l->is_list) {
+      for (auto const &k : l->kids) dump_vars.push_back(k.second->leaf);
+    } else {
+      std::string v = l->leaf;
+      for (size_t b = 0; b <= v.size();) {
+        size_t e = v.find(':', b);
+        if (e == std::string::npos) e = v.size();
+        if (e > b) dump_vars.push_back(v.substr(b, e - b));
+        b = e + 1;
+      }
+    }
+  }
+  p_lexp_t rl = parse_lexp(a.get_str("rtc", "(be=hip)"));
+  nesi_init_arg_t ra(rl);
+  const std::string be = ra.get_str("be", "hip");
+  if (be != "hip") unsup_err("rtc mode: backend be=" + be + " is not built here (this backend provides be=hip)");
+  const int device = (int)ra.get_u32("device", 0);
+  ra.check_unused();
+  a.check_unused();
+  if (!rtc) {
+    rtc = make_hip_compute(device);
+    rtc->init();
+  }
+  init_with_rtc(cp_, rtc);
+}
+
+void conv_pipe_fwd_t::set_det_drop_seed(uint32_t const &det_drop_seed_) {  // src/rtc_fwd.cc:91-99
+  det_drop_seed = det_drop_seed_;
+  for (uint32_t i : dropout_cixs) {
+    auto it = calls.at(i).rfc.arg_map.find("det_drop_seed");
+    if (it == calls.at(i).rfc.arg_map.end()) rt_err("set_det_drop_seed: dropout call without a seed argument");
+    it->second = rtc_arg_t::u32(det_drop_seed_);
+  }
+}
+
+// src/rtc_fwd.cc:535-577
+void conv_pipe_fwd_t::run_fwd(vect_string const &to_set_vns, p_map_str_p_nda_t const &fwd,
+                              vect_string const &to_get_vns) {
+  if (!rtc) rt_err("conv_pipe_fwd_t::run_fwd before init");
+  if (!fwd) rt_err("conv_pipe_fwd_t::run_fwd: null fwd map");
+  if (enable_double_run)
+    for (auto const &c : calls) rtc->run(c.rfc);
+  rtc->finish_and_sync();
+  for (auto const &vn : to_set_vns) {  // copy sources in
+    auto it = fwd->find(vn);
+    if (it == fwd->end() || !it->second) rt_err("run_fwd: no input nda named '" + vn + "'");
+    if (!declared.count(vn)) rt_err("run_fwd: '" + vn + "' is not a var of this net");
+    rtc->copy_nda_to_var(vn, it->second);
+  }
+  rtc->finish_and_sync();
   rtc->release_per_call_id_data();
   std::vector<uint32_t> ids;
   for (auto const &c : calls) ids.push_back(rtc->run(c.rfc));
   rtc->finish_and_sync();
+  for (auto const &vn : to_get_vns) {  // copy requested vars out
+    if (!declared.count(vn))
+      rt_err("run_fwd: blob '" + vn + "' has no var (a rewrite keeps it only inside another op's output)");
+    (*fwd)[vn] = rtc->create_nda_from_var(vn);
+  }
   times.clear();
   for (size_t i = 0; i < calls.size(); ++i) {
     layer_time_t t;
     t.tag = calls[i].tag;
     t.func = calls[i].rfc.rtc_func_name;
-    t.ms = rtc->get_dur(ids[i], ids[i]);
+    t.ms = enable_prof ? rtc->get_dur(ids[i], ids[i]) : 0.0;
     t.flops = calls[i].flops;
     times.push_back(t);
   }
+  if (!per_call_fn.empty()) {
+    FILE *f = fopen(per_call_fn.c_str(), "w");
+    if (!f) rt_err("cannot write per_call_fn " + per_call_fn);
+    const double dur = ids.empty() ? 0.0 : rtc->get_dur(ids.front(), ids.back());
+    fprintf(f, "net.args.runtime=%.9g\n", dur / 1000.0);
+    for (auto const &t : times)
+      fprintf(f, "per_layer_time['%s']=per_layer_time.get('%s',0.0) + %.9g # %s \n", t.tag.c_str(), t.tag.c_str(),
+              t.ms / 1000.0, t.func.c_str());
+    fclose(f);
+  }
+  stats_map.clear();
+  if (enable_stats) {
+    for (auto const &vn : to_get_vns) {
+      nda_t const &n = *fwd->at(vn);
+      double mn = 0, mx = 0, sum = 0;
+      const uint64_t cnt = n.dims.elems();
+      for (uint64_t i = 0; i < cnt; ++i) {
+        const double v = n.elems()[i];
+        mn = i ? std::min(mn, v) : v;
+        mx = i ? std::max(mx, v) : v;
+        sum += v;
+      }
+      stats_map[vn + "_min"] = mn;
+      stats_map[vn + "_max"] = mx;
+      stats_map[vn + "_sum"] = sum;
+      stats_map[vn + "_cnt"] = (double)cnt;
+    }
+  }
+  graph_ms = graph_reps ? time_fwd_graph(graph_reps) : 0.0;
+  rtc->release_per_call_id_data();
+  rtc->finish_and_sync();
+}
+
+// src/rtc_fwd.cc:140-161: dumped vars and stats; plus (enable_prof) the per-call times of the
+// last forward and, with graph_reps, the forward as one replayed hipGraph
+std::string conv_pipe_fwd_t::get_info_log(void) {
+  std::string ret;
+  char buf[512];
+  if (enable_prof) {
+    double flops = 0;
+    for (auto const &t : times) {
+      char rate[32] = "";
+      if (t.flops > 0 && t.ms > 0) snprintf(rate, sizeof(rate), "%.1f GFLOP/s", t.flops / t.ms / 1e6);
+      snprintf(buf, sizeof(buf), "  %-28s %-34s %9.4f ms %s\n", t.tag.c_str(), t.func.c_str(), t.ms, rate);
+      ret += buf;
+      flops += t.flops;
+    }
+    snprintf(buf, sizeof(buf), "forward %.4f ms  conv GFLOP %.3f  %.1f GFLOP/s\n", sum_ms(), flops / 1e9,
+             sum_ms() > 0 ? flops / sum_ms() / 1e6 : 0.0);
+    ret += buf;
+    if (graph_reps) {
+      snprintf(buf, sizeof(buf), "forward as one hipGraph (%zu calls, %u replays) %.4f ms  %.1f GFLOP/s\n",
+               times.size(), graph_reps, graph_ms, graph_ms > 0 ? flops / graph_ms / 1e6 : 0.0);
+      ret += buf;
+    }
+  }
+  for (auto const &vn : dump_vars) {
+    p_nda_t n = rtc->create_nda_from_var(vn);
+    ret += "dumping var '" + vn + "'\n";
+    for (uint64_t i = 0; i < n->dims.elems(); ++i) {
+      snprintf(buf, sizeof(buf), "[%llu]: %.9g\n", (unsigned long long)i, n->elems()[i]);
+      ret += buf;
+    }
+  }
+  for (auto const &kv : stats_map) {
+    snprintf(buf, sizeof(buf), "%s=%.9g\n", kv.first.c_str(), kv.second);
+    ret += buf;
+  }
+  return ret;
 }
 
 double conv_pipe_fwd_t::time_fwd_graph(uint32_t reps) {

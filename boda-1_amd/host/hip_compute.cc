@@ -138,7 +138,7 @@ struct hip_compute_t : public rtc_compute_t {
   void compile(std::vector<rtc_func_info_t> const &fis, rtc_compile_opts_t const &opts) override {
     static const std::set<std::string> kinds = {"hip_sgemm", "hip_conv",  "hip_xpose_filts", "hip_pool",
                                                 "hip_lrn",   "hip_relu",  "hip_copy",        "hip_affine",
-                                                "hip_eltwise", "hip_softmax"};
+                                                "hip_eltwise", "hip_softmax", "hip_dropout"};
     std::string src = cucl_hip_prelude;
     std::vector<std::string> jit_names;
     for (auto const &fi : fis) {
@@ -263,6 +263,13 @@ struct hip_compute_t : public rtc_compute_t {
                fn);
     } else if (kind == "hip_relu") {
       bh_check(bh_relu_inplace(ctx, arg_ptr(rfc, "x"), arg_dims(rfc, "x").elems()), fn);
+    } else if (kind == "hip_dropout") {  // test/rtc/dropout.cucl: inout, dropout_ratio, det_drop_seed
+      // det_drop_seed is a by-value CALL argument (set_det_drop_seed rewrites it per forward)
+      auto sd = rfc.arg_map.find("det_drop_seed");
+      if (sd == rfc.arg_map.end() || !sd->second.has_v) rt_err(fn + ": call lacks the det_drop_seed value");
+      bh_check(bh_dropout_inplace(ctx, arg_ptr(rfc, "inout"), arg_dims(rfc, "inout").elems(), fv("dropout_ratio"),
+                                  (uint32_t)sd->second.v),
+               fn);
     } else if (kind == "hip_copy") {  // channel slab copy: Concat / Split / Dropout-as-copy
       uint32_t B, C, H, W, OB, OC_, OH, OW;
       nchw("in", B, C, H, W);

@@ -195,6 +195,10 @@ int bh_lrn_fwd_nchw(bh_ctx *ctx, const float *in, float *out, float *out_scale_b
                     uint32_t H, uint32_t W, uint32_t local_size, float alpha, float beta, float k);
 /* ReLU in place (test/rtc/relu.cucl); x 16-byte aligned, n elements. */
 int bh_relu_inplace(bh_ctx *ctx, float *x, uint64_t n);
+/* Deterministic dropout in place (test/rtc/dropout.cucl; the rtc mode's Dropout, seeded by
+ * has_conv_fwd_t::set_det_drop_seed, src/rtc_fwd.cc:91-99,348-358): x[i] = murmur3 finalizer of
+ * (i + det_drop_seed) > U32_MAX * ratio ? x[i] / (1 - ratio) : 0; 0 < ratio < 1. */
+int bh_dropout_inplace(bh_ctx *ctx, float *x, uint64_t n, float ratio, uint32_t det_drop_seed);
 /* Softmax over channels per pixel (test/rtc/softmax.cucl). */
 int bh_softmax_chans(bh_ctx *ctx, const float *in, float *prob, uint32_t B, uint32_t C, uint32_t H, uint32_t W);
 /* Channel-slab copy between NCHW tensors of equal H*W = HW: out[img][oc0 + c] =

@@ -91,6 +91,24 @@ def relu(x):
     return np.where(x <= 0, F32(0), x).astype(F32)
 
 
+def dropout(x, ratio, seed):
+    """test/rtc/dropout.cucl:7-19: element i (flat index) kept and scaled by 1 / (1 - ratio) iff the
+    murmur3 finalizer of (i + det_drop_seed) exceeds U32_MAX * ratio (the ratio is substituted
+    into the kernel text, so both products are double), else 0."""
+    m = 0xffffffff
+    h = (np.arange(x.size, dtype=np.uint64) + np.uint64(seed)) & m
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & m
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & m
+    h ^= h >> 16
+    r = float(F32(ratio))
+    thresh = int(4294967295.0 * r)
+    scale = F32(1.0 / (1.0 - r))
+    flat = x.reshape(-1).astype(F32)
+    return np.where(h > thresh, flat * scale, F32(0)).astype(F32).reshape(x.shape)
+
+
 def softmax(x):
     """test/rtc/softmax.cucl:8-22: max starts at 0, exp(x - max), divide by the sum (channel
     order)."""

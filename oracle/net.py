@@ -90,8 +90,9 @@ class _S:  # conv shape for oracle.conv_ref
         self.__dict__.update(kw)
 
 
-def forward(plan, x):
-    """Run the plan on input x (B x C x H x W float32); returns {blob: array}."""
+def forward(plan, x, drop_seed=0):
+    """Run the plan on input x (B x C x H x W float32); returns {blob: array}. Dropout ops
+    (plans read with --det-dropout) use the rtc mode's deterministic mask seeded by drop_seed."""
     check_dims(plan)
     blobs = {plan["inputs"][0]["name"]: x.astype(F32)}
     for op in plan["ops"]:
@@ -110,6 +111,8 @@ def forward(plan, x):
             out = orc.conv_ref(np.ascontiguousarray(a).reshape(-1), f, b, s, op["relu"]).reshape(B, OC, s.OH, s.OW)
         elif t == "ReLU":
             out = L.relu(a)
+        elif t == "Dropout":  # in place (src/rtc_fwd.cc:348-358)
+            out = L.dropout(a, op["ratio"], drop_seed)
         elif t == "Pooling":
             ky, kx = (H, W) if op["global"] else op["k"]
             sy, sx = (1, 1) if op["global"] else op["s"]

@@ -199,3 +199,26 @@ def test_conv_residual_epilogue(dev, s, relu):
     if relu:
         exp = np.where(exp < 0, np.float32(0), exp)
     np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("s", [ops.ConvShape(1, 128, 4, 4, 1024, 4, 4, 1, 1, 0, 0),     # fcv route (ipconv)
+                               ops.ConvShape(1, 1024, 1, 1, 1000, 1, 1, 1, 1, 0, 0),    # fcv route (FC)
+                               ops.ConvShape(1, 528, 14, 14, 128, 1, 1, 1, 1, 0, 0),    # gvo route (1x1)
+                               ops.ConvShape(1, 528, 4, 4, 128, 1, 1, 1, 1, 0, 0)])     # gvo route
+@pytest.mark.parametrize("which", ["in", "filts", "both"])
+def test_dword_aligned_pointers_on_vector_routes(dev, s, which):
+    """A dword-aligned but not 16-B-aligned input or filter pointer on a shape whose table route
+    needs 16-B loads (fcv, gvo) computes through a fallback kernel instead of failing."""
+    import boda_hip as bh
+    ni, nf = s.B * s.IC * s.H * s.W, s.OC * s.K
+    bi, bf = dev.alloc_floats(ni + 4), dev.alloc_floats(nf + 4)
+    b, o = dev.alloc_floats(s.OC), dev.alloc_floats(s.B * s.OC * s.OH * s.OW)
+    vi = bh.DevBuf(dev, bi.ptr + (4 if which in ("in", "both") else 0), ni * 4)
+    vf = bh.DevBuf(dev, bf.ptr + (4 if which in ("filts", "both") else 0), nf * 4)
+    dev.gen_data(GEN_CONV_IN, vi, [s.B, s.IC, s.H, s.W], 5)
+    dev.gen_data(GEN_CONV_FILTS, vf, [s.OC, s.IC, s.KY, s.KX], 5)
+    dev.gen_data(GEN_CONV_BIASES, b, [s.OC], 5)
+    dev.conv(vi, vf, b, o, s, 1)
+    check_vs_oracle(o.download(), s)
+    for x in (bi, bf, b, o):
+        x.free()

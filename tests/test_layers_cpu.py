@@ -48,3 +48,31 @@ def test_softmax_and_relu():
     e = np.exp([-3.0, -2.0, 0.0])
     np.testing.assert_allclose(p, e / e.sum(), rtol=1e-6)
     np.testing.assert_array_equal(L.relu(x)[0, :, 0, 0], [0, 0, 2])
+
+
+def _murmur_fmix32(h):
+    """Reference scalar form (test/rtc/dropout.cucl:12-17), for the known answers below."""
+    h &= 0xffffffff
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & 0xffffffff
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & 0xffffffff
+    h ^= h >> 16
+    return h
+
+
+def test_dropout_known_answer():
+    x = np.arange(1, 65, dtype=np.float32).reshape(1, 4, 4, 4)
+    for seed in (0, 7, 0xfffffff0):
+        got = L.dropout(x, 0.5, seed).reshape(-1)
+        for i, v in enumerate(x.reshape(-1)):
+            keep = _murmur_fmix32(i + seed) > 2147483647  # (uint32)(U32_MAX * 0.5)
+            assert got[i] == (v * np.float32(2.0) if keep else 0.0), (seed, i)
+        kept = (got != 0).mean()
+        assert 0.3 < kept < 0.7
+    # murmur3's finalizer maps 0 to 0: element 0 at seed 0 is always dropped
+    assert L.dropout(x, 0.25, 0).reshape(-1)[0] == 0
+    # ratio 0.25: survivors scaled by 4/3 in fp32
+    y = L.dropout(x, 0.25, 3).reshape(-1)
+    nz = y != 0
+    np.testing.assert_array_equal(y[nz], x.reshape(-1)[nz] * np.float32(1.0 / 0.75))

@@ -109,3 +109,32 @@ def test_exec_plan_folds_and_slabs():
     assert exec_plan("googlenet_conv", "--no-inplace-concat") == []
     for n in ("alexnet_ng_conv", "nin_imagenet", "vgg_19"):
         assert exec_plan(n) == []
+
+
+def test_mode_args_checked_before_the_backend():
+    """has_conv_fwd_t init(cp, nia): every mode argument must be used (the reference's
+    init_and_check_unused), and the rtc mode only provides be=hip -- both raised by init before
+    any backend exists (no GPU needed)."""
+    pt = os.path.join(NETS, "alexnet_ng_conv.prototxt")
+    r = subprocess.run([BIN, "--net", pt, "--img", "1", "--mode-args", "(enable_stats=1,bogus_opt=3)"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "unused mode arguments: bogus_opt" in r.stderr, r.stderr
+    r = subprocess.run([BIN, "--net", pt, "--img", "1", "--mode-args", "(enable_prof=x)"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "not a uint32" in r.stderr, r.stderr
+
+
+def test_det_dropout_plan():
+    """--det-dropout keeps the in-place Dropout layers (ratio in the plan); by default they are the
+    identity of the TEST phase and dropped."""
+    p0 = plan("alexnet_ng_conv", 1)
+    assert not [o for o in p0["ops"] if o["type"] == "Dropout"]
+    pt = os.path.join(NETS, "alexnet_ng_conv.prototxt")
+    r = subprocess.run([BIN, "--net", pt, "--img", "1", "--plan-json", "--det-dropout", "5"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    p1 = json.loads(r.stdout)
+    drops = [o for o in p1["ops"] if o["type"] == "Dropout"]
+    assert [o["tag"] for o in drops] == ["drop6", "drop7"] and all(o["ratio"] == 0.5 for o in drops)
+    assert all(o["tops"] == o["bots"] for o in drops)
+    assert "drop6" not in " ".join(p1["ignored"])
