@@ -23,7 +23,7 @@ GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5
 EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_destroy", "bh_plat_tag",
            "bh_get_stream", "bh_alloc", "bh_free", "bh_memset0", "bh_h2d", "bh_d2h", "bh_sync",
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
-           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_cfg_name",
+           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_set_policy", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
            "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
@@ -98,6 +98,7 @@ def lib():
         L.bh_graph_launch.argtypes = [c_vp, ctypes.c_int]
         L.bh_graph_destroy.argtypes = [c_vp, ctypes.c_int]
         L.bh_tune_set.argtypes = [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.bh_tune_set_policy.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
         L.bh_tune_cfg_name.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
         L.bh_jit_build.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t)]
@@ -276,6 +277,10 @@ class Device:
 
     def tune_set(self, op_kind, cfg_index=-1, splits=0):
         _check(lib().bh_tune_set(self.ctx, op_kind, cfg_index, splits))
+
+    def tune_set_policy(self, op_kind, wt=-1):
+        """Output store policy override: 1 write-through, 0 write-back, -1 the table's choice."""
+        _check(lib().bh_tune_set_policy(self.ctx, op_kind, wt))
 
     def sgemm(self, a, b, c, M, N, K):
         _check(lib().bh_sgemm_kmajor(self.ctx, a.ptr, b.ptr, c.ptr, M, N, K))

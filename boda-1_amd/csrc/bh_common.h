@@ -22,6 +22,7 @@ struct bh_ctx {
   int ovr_cfg[2] = {-1, -1};  // tuning override per op (0 sgemm, 1 conv); -1 = table/heuristic
   uint32_t ovr_splits[2] = {0, 0};
   int ovr_red[2] = {0, 0};
+  int ovr_wt[2] = {-1, -1};  // output store policy override (-1 = the table's / heuristic's)
   std::vector<hipGraphExec_t> graphs;  // captured launch sequences
   void *stamps = nullptr;              // device timestamp slots (bh_stamp)
   hipEvent_t t_start = nullptr;        // bh_time_next_call: events for the next call's
@@ -119,6 +120,7 @@ int grow_buffer(bh_ctx *ctx, void *&buf, size_t &have, size_t want, bool zero, c
 namespace bh {
 int launch_gen_data(bh_ctx *ctx, int kind, float *dst, const uint32_t dims[4], uint32_t mode, float vi);
 int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t M, uint32_t N, uint32_t K);
+int tune_set_wt(bh_ctx *ctx, int op, int wt);
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
                 float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                 uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0,

@@ -845,6 +845,7 @@ struct choice_t {
   int cfg = -1;
   uint32_t splits = 0;  // 0 = plan
   int red = 0;          // split-K combine: 0 = plan, 1 = reduce kernel, 2 = in-kernel last arriver
+  int wt = 0;           // output stores write through (GemmArgs::wt)
 };
 std::map<std::string, choice_t> g_tune;
 std::once_flag g_tune_once;
@@ -884,6 +885,8 @@ void load_tuning() {
     ch.splits = (uint32_t)strtoul(l.c_str() + s + 8, nullptr, 10);
     size_t r = l.find(" red=");
     if (r != std::string::npos) ch.red = l[r + 5] == 'k' ? 1 : 2;
+    size_t w = l.find(" wt=");
+    if (w != std::string::npos) ch.wt = l[w + 4] == '1' ? 1 : 0;
     if (ch.cfg >= 0) g_tune[key] = ch;
   }
   fclose(f);
@@ -922,17 +925,18 @@ choice_t heuristic(int op, const uint32_t *d, bool ring = true, bool direct = tr
 }
 
 choice_t choose(bh_ctx *ctx, int op, const uint32_t *d) {
+  choice_t ch;
   if (ctx && ctx->ovr_cfg[op] >= 0) {
-    choice_t ch;
     ch.cfg = ctx->ovr_cfg[op];
     ch.splits = ctx->ovr_splits[op];
     ch.red = ctx->ovr_red[op];
-    return ch;
+  } else {
+    std::call_once(g_tune_once, load_tuning);
+    auto it = g_tune.find(shape_key(op, d));
+    ch = it != g_tune.end() ? it->second : heuristic(op, d);
   }
-  std::call_once(g_tune_once, load_tuning);
-  auto it = g_tune.find(shape_key(op, d));
-  if (it != g_tune.end()) return it->second;
-  return heuristic(op, d);
+  if (ctx && ctx->ovr_wt[op] >= 0) ch.wt = ctx->ovr_wt[op];  // policy override (tuner)
+  return ch;
 }
 
 uint32_t resolve_splits(cfg_t const &c, choice_t const &ch, uint32_t M, uint32_t N, uint32_t K, uint32_t ncu) {
@@ -1056,7 +1060,11 @@ void conv_dims(const uint32_t *d, uint32_t &M, uint32_t &N, uint32_t &K) {
   K = IC * KY * KX;
 }
 
+std::string describe_cfg(int op, const uint32_t *d, choice_t const &ch);
 std::string describe(int op, const uint32_t *d, choice_t const &ch) {
+  return describe_cfg(op, d, ch) + (ch.wt ? "_wt" : "");
+}
+std::string describe_cfg(int op, const uint32_t *d, choice_t const &ch) {
   cfg_t const &c = cfgs(op)[ch.cfg];
   uint32_t M, N, K;
   std::string s;
@@ -1105,6 +1113,12 @@ int tune_set(bh_ctx *ctx, int op, int cfg, int splits) {
   return BH_OK;
 }
 
+int tune_set_wt(bh_ctx *ctx, int op, int wt) {
+  if (op < 0 || op > 1) return fail(BH_ERR, "tune_set_wt: op must be 0 (sgemm) or 1 (conv)");
+  ctx->ovr_wt[op] = wt < 0 ? -1 : (wt ? 1 : 0);
+  return BH_OK;
+}
+
 int tune_cfg_name(int op, int cfg, std::string &out) {
   if (op < 0 || op > 1) return fail(BH_ERR, "op must be 0 (sgemm) or 1 (conv)");
   if (cfg < 0 || cfg >= (int)cfgs(op).size()) return fail(BH_UNSUP, "no such config");
@@ -1126,6 +1140,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
   p.cvec = (N % 4 == 0) && ((uintptr_t)c % 16 == 0);
   uint32_t d[3] = {M, N, K};
   choice_t ch = choose(ctx, 0, d);
+  p.wt = ch.wt && fits_buffer((uint64_t)M * N * 4);
   if (getenv("BH_EXP_RING_DWORD_B") && vec && cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0])  // experiment
     return launch_gemm(ctx, 0, ch, A_KSCALAR, B_KSCALAR, p, "sgemm");
   if (!vec && (!cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0] || cfgs(0)[ch.cfg].name[0] == 'r')) ch = heuristic(0, d, false);
@@ -1170,6 +1185,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   const bool avec = (K % 4 == 0) && ((uintptr_t)filts % 16 == 0);
   uint32_t d[11] = {B, IC, H, W, OC, KY, KX, sy, sx, py, px};
   choice_t ch = choose(ctx, 1, d);
+  p.wt = ch.wt;  // the output fits a 2 GiB buffer (checked above)
   if (no_dc && cfgs(1)[ch.cfg].dc) ch = heuristic(1, d, true, false);
   const bool first = !repacked;
   if (cfgs(1)[ch.cfg].gv && !cfgs(1)[ch.cfg].packA) {

@@ -49,6 +49,8 @@ struct GemmArgs {
   uint32_t tiles_m, tiles_n;
   int relu;
   int cvec;  // dense C rows can take TN-wide vector stores
+  int wt;    // output stores write through (sc1): the output leaves L2 during the kernel instead of
+             // at the next kernel boundary (set only when the output fits a 2 GiB buffer)
   const float *res;  // conv only, may be null: out = relu(conv + bias + res), res laid out like out
   // implicit im2col (B_IM2COL / B_IM1X1); N = B*OH*OW, K = IC*KY*KX
   uint32_t H, W, KX, KYX, sy, sx, py, px, OW, OHW, HW, ICHW, OCOHW;
@@ -121,6 +123,37 @@ __device__ __forceinline__ float vget(const typename fvec<N>::t &v, int i) {
   else return v[i];
 }
 
+constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
+// Final output stores: write-through. Dirty L2 lines left at the end of a kernel are written back
+// at the kernel boundary, before the next launch in the stream starts (MI355X_MICROARCH.md,
+// boundary row: + bytes / ~6 TB/s); written through during the kernel they overlap the compute.
+#ifndef BH_AUX_OUT
+#define BH_AUX_OUT 0
+#endif
+constexpr int AUX_OUT = BH_AUX_OUT;
+
+// Output stores under the call's policy (p.wt, wave-uniform): write-through (sc1) or AUX_OUT
+__device__ __forceinline__ void out_store4(const GemmArgs &p, __amdgpu_buffer_rsrc_t r, uint32_t off, f32x4v v) {
+  const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v);
+  if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX_SC1);
+  else __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX_OUT);
+}
+__device__ __forceinline__ void out_store1(const GemmArgs &p, __amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_SC1);
+  else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_OUT);
+}
+// element o of p.c (plain stores, or buffer stores through sc1 when p.wt)
+__device__ __forceinline__ void out_elem4(const GemmArgs &p, size_t o, f32x4v v) {
+  if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                   make_rsrc(p.c, 0x7fffff00u), (uint32_t)(o * 4), 0, AUX_SC1);
+  else *(f32x4v *)&p.c[o] = v;
+}
+__device__ __forceinline__ void out_elem1(const GemmArgs &p, size_t o, float v) {
+  if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), make_rsrc(p.c, 0x7fffff00u),
+                                                  (uint32_t)(o * 4), 0, AUX_SC1);
+  else p.c[o] = v;
+}
+
 // Split-K slabs are summed in fixed order s = 0..S-1 (bitwise reproducible whoever
 // combines: the reduce kernel or a tile's last-arriving block).
 // Bias, ReLU and store of one float4 chunk c (tile elements 4c..4c+3, row-major BM x BN)
@@ -153,7 +186,7 @@ __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) sum[t] = (p.relu && sum[t] < 0.0f) ? 0.0f : sum[t];
-    *(f32x4v *)&p.c[o] = sum;
+    out_elem4(p, o, sum);
     return;
   }
 #pragma unroll
@@ -165,9 +198,9 @@ __device__ __forceinline__ void finish_store_b(const GemmArgs &p, uint32_t tile_
       const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s);
       const size_t o = (size_t)img * p.OCOHW + (size_t)m * p.OHW + (n - img * p.OHW);
       if (p.res) x += p.res[o];
-      p.c[o] = (p.relu && x < 0.0f) ? 0.0f : x;
+      out_elem1(p, o, (p.relu && x < 0.0f) ? 0.0f : x);
     } else {
-      p.c[(size_t)m * p.ldc + n] = (p.relu && x < 0.0f) ? 0.0f : x;
+      out_elem1(p, (size_t)m * p.ldc + n, (p.relu && x < 0.0f) ? 0.0f : x);
     }
   }
 }
@@ -180,14 +213,7 @@ __device__ __forceinline__ void finish_store(const GemmArgs &p, uint32_t tile_m,
   finish_store_b<IMODE>(p, tile_m, tile_n, c, sum, bias_lds ? bias_lds[row] : (p.bias ? p.bias[m] : 0.0f));
 }
 
-constexpr int AUX_SC1 = 16;  // cache-policy bits: sc1 (write-through stores / L1-bypassing loads)
-// Final output stores: write-through. Dirty L2 lines left at the end of a kernel are written back
-// at the kernel boundary, before the next launch in the stream starts (MI355X_MICROARCH.md,
-// boundary row: + bytes / ~6 TB/s); written through during the kernel they overlap the compute.
-#ifndef BH_AUX_OUT
-#define BH_AUX_OUT 0
-#endif
-constexpr int AUX_OUT = BH_AUX_OUT;
+
 
 // Split-K combine of one float4 chunk c for the reduce kernel (after a kernel boundary,
 // so plain loads): the S slabs summed in fixed order, four in flight.

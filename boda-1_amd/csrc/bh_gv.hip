@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void fcv_kernel(GemmArgs p) {
         const size_t o = (size_t)b * p.OCOHW + m;
         float v = acc[r][b] + (p.bias ? p.bias[m] : 0.0f);
         if (p.res) v += p.res[o];
-        p.c[o] = (p.relu && v < 0.0f) ? 0.0f : v;
+        out_elem1(p, o, (p.relu && v < 0.0f) ? 0.0f : v);
       }
     }
 }

@@ -138,6 +138,9 @@ __global__ __launch_bounds__(NW * 64) void k1s_kernel(GemmArgs p) {
     else vm_wait<(Q - 2) * SC>();
     if (u0) {
       __syncthreads();
+#ifdef BH_KTRACE
+      if (cq == 0 && r == 0) KT(1);
+#endif
 #pragma unroll
       for (int s = 0; s < PF; ++s) frag(wf[s], cq + r, s);
     }
@@ -227,8 +230,7 @@ __global__ __launch_bounds__(NW * 64) void k1s_kernel(GemmArgs p) {
           for (int e = 0; e < 4; ++e) y[e] = (p.relu && y[e] < 0.0f) ? 0.0f : y[e];
           // always issued (dropped where the quad goes element by element): every unit has at
           // least S vector stores, which the loop's waits count on
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y),
-                                                 rso, quad && (DBG & 4) == 0 ? o : OOB, 0, AUX_OUT);
+          out_store4(p, rso, quad && (DBG & 4) == 0 ? o : OOB, y);
           if (!quad && (oc < p.M) && (pu < npu)) {
             // a quad past its image or the op, or a residual epilogue: element by element (more
             // VMEM instructions than counted only make the waits stricter)
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(NW * 64) void k1s_kernel(GemmArgs p) {
               float z = v[e];
               if (p.res) z += ld1(rsr, oe);
               z = (p.relu && z < 0.0f) ? 0.0f : z;
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, oe, 0, AUX_OUT);
+              out_store1(p, rso, oe, z);
             }
           }
         }

@@ -472,6 +472,11 @@ int bh_tune_set(bh_ctx *c, int op, int cfg_index, int splits) {
   return bh::tune_set(c, op, cfg_index, splits);
 }
 
+int bh_tune_set_policy(bh_ctx *c, int op, int wt) {
+  BH_ENTER(c);
+  return bh::tune_set_wt(c, op, wt);
+}
+
 int bh_tune_cfg_name(int op, int cfg_index, char *buf, size_t n) {
   if (!buf || !n) return bh::fail(BH_ERR, "null buffer");
   std::string s;

@@ -248,6 +248,11 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t buflen);
  * splits combined in-kernel by each tile's last-arriving block, -n = n splits
  * combined by a separate reduce kernel. Both combines sum in a fixed order. */
 int bh_tune_set(bh_ctx *ctx, int op, int cfg_index, int splits);
+/* force the output store policy of every later call of op on this context: wt 1 = the outputs
+ * are written through (sc1) during the kernel instead of left dirty in L2 for the next kernel
+ * boundary to write back; 0 = write-back; -1 = back to the table's / heuristic's choice
+ * (tuning tables carry it as " wt=1"). Results are bit-identical either way. */
+int bh_tune_set_policy(bh_ctx *ctx, int op, int wt);
 /* name of tile configuration cfg_index; BH_UNSUP past the last one */
 int bh_tune_cfg_name(int op, int cfg_index, char *buf, size_t buflen);
 

@@ -110,6 +110,10 @@ def main():
     ap.add_argument("--key-re", default="", help="sweep only ops whose table key ('conv B IC H W ...') matches")
     ap.add_argument("--only-untuned", action="store_true", help="sweep only ops the --out table has no entry "
                     "for (use with --merge)")
+    ap.add_argument("--wt", choices=["try", "off", "only"], default="try",
+                    help="output store policy: try write-through (wt=1) on each op's best config and keep it if "
+                         "faster by --wt-gain; 'only': keep the --out table's configs, sweep just the policy")
+    ap.add_argument("--wt-gain", type=float, default=0.01)
     args = ap.parse_args()
     global TIMING
     TIMING = args.timing
@@ -119,7 +123,7 @@ def main():
     names = {0: boda_hip.tune_cfg_names(0), 1: boda_hip.tune_cfg_names(1)}
     table, results = {}, []
     prev = {}
-    if args.cfg_re and os.path.exists(args.out):
+    if (args.cfg_re or args.wt == "only") and os.path.exists(args.out):
         for l in open(args.out):
             m = re.match(r"(.*) cfg=(\S+) splits=(\d+) red=(\w)", l)
             if m:
@@ -182,6 +186,8 @@ def main():
                         cand.append((ci, S))
                         if S > 1:
                             cand.append((ci, -S))  # same split, separate reduce kernel
+            if args.wt == "only":
+                cand = []
             if key in prev and prev[key][0] in names[kind]:
                 cand.append((names[kind].index(prev[key][0]), prev[key][1]))
             for ci, S in cand:
@@ -194,22 +200,39 @@ def main():
                 if t < best[0]:
                     best = (t, ci, S)
             dev.tune_set(kind, -1, 0)
-            wl.free()
             results.append({"key": key, "cfg": "default", "splits": 0, "ms": t_def})
             if key in prev:  # keep the table's choice unless clearly beaten in this run
                 pt = [x["ms"] for x in results if x["key"] == key and x["cfg"] == prev[key][0]
                       and x["splits"] == prev[key][1]]
                 if pt and best[0] >= (1 - args.min_gain) * pt[0]:
                     best = (pt[0], names[kind].index(prev[key][0]), prev[key][1])
+            wt = 0
+            if best[1] >= 0 and args.wt != "off":
+                # the same route with write-through output stores (bit-identical results)
+                dev.tune_set(kind, best[1], best[2])
+                dev.tune_set_policy(kind, 1)
+                try:
+                    t = time_op(dev, wl, 0, args.reps)
+                    dev.tune_set_policy(kind, 0)
+                    t0 = time_op(dev, wl, 0, args.reps)  # the same route timed again, write-back
+                    results.append({"key": key, "cfg": names[kind][best[1]], "splits": best[2], "wt": 1, "ms": t,
+                                    "ms_wb": t0})
+                    if t < (1 - args.wt_gain) * min(t0, best[0]):
+                        best, wt = (t, best[1], best[2]), 1
+                except boda_hip.UnsupportedError:
+                    pass
+                dev.tune_set_policy(kind, -1)
+                dev.tune_set(kind, -1, 0)
+            wl.free()
             if best[1] >= 0:
-                table[key] = (names[kind][best[1]], best[2], best[0], t_def)
+                table[key] = (names[kind][best[1]], best[2], best[0], t_def, wt)
             rf = runner.roofline_secs(s) * 1e3
             print("%-48s default %.4f ms  best %s S=%+d %.4f ms  roofline %.4f ms (%.0f%%)" % (
                 key, t_def, names[kind][best[1]] if best[1] >= 0 else "default", best[2], best[0], rf,
                 100 * rf / best[0]), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
-    lines = {k: "%s cfg=%s splits=%d red=%s" % (k, cn, abs(S), "k" if S < 0 else "i")
-             for k, (cn, S, t, td) in table.items()}
+    lines = {k: "%s cfg=%s splits=%d red=%s%s" % (k, cn, abs(S), "k" if S < 0 else "i", " wt=1" if wt else "")
+             for k, (cn, S, t, td, wt) in table.items()}
     if args.merge and os.path.exists(args.out):
         old = {}
         for l in open(args.out):
