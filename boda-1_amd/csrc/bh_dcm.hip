@@ -274,7 +274,8 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
               x[e] += bb;
               x[e] = (p.relu && x[e] < 0.0f) ? 0.0f : x[e];
             }
-            out_store4(p, rso, o, x);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, x),
+                                                   rso, o, 0, AUX_OUT);
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(256 * WO) void dcm_kernel(GemmArgs p) {
               float y = x[e] + bb;
               if (p.res) y += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
               y = (p.relu && y < 0.0f) ? 0.0f : y;
-              out_store1(p, rso, o, y);
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, y), rso, o, 0, AUX_OUT);
             }
           }
         }

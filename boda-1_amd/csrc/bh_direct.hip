@@ -158,14 +158,16 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     const uint32_t px = dpx + (uint32_t)(32 * tn + 8 * gq);
     const uint32_t off = dbase[t] + (uint32_t)(32 * tn + 8 * gq) * 4u;
     if (px + 4 <= dhw) {
-      out_store4(p, rso, off, dval[q]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
+                                             rso, off, 0, AUX_OUT);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // (a scalar first: __builtin_bit_cast of a vector component made hipcc store component 0
         // four times -- caught by the 224-wide, OH*OW % 4 == 2 test shapes)
         const float xe = dval[q][e];
-        out_store1(p, rso, oob_unless(px + (uint32_t)e < dhw, off + 4u * (uint32_t)e), xe);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, xe), rso,
+                                              oob_unless(px + (uint32_t)e < dhw, off + 4u * (uint32_t)e), 0, AUX_OUT);
       }
     }
   };
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
             float x = acc[t][tn][r] + bb;
             if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
             x = (p.relu && x < 0.0f) ? 0.0f : x;
-            out_store1(p, rso, o, x);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, AUX_OUT);
           }
       }
     }
