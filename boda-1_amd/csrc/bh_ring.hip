@@ -25,10 +25,12 @@
 namespace bhk {
 namespace {
 
-template <int TM, int TN, int BK, int D, int BLD, int SPL>
-__global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
-  constexpr int NW = 4, NT = 256;
-  constexpr int BM = 64 * TM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
+// WGM: waves along M (2: 4 waves as 2 x 2; 4: 8 waves as 4 x 2, two per SIMD sharing one
+// stage: a 256-row SGEMM tile halves the B-panel DMA per MFMA of the 128-row tile)
+template <int TM, int TN, int BK, int D, int BLD, int SPL, int WGM = 2>
+__global__ __launch_bounds__(128 * WGM) void ring_kernel(GemmArgs p) {
+  constexpr int NW = 2 * WGM, NT = 64 * NW;
+  constexpr int BM = 32 * TM * WGM, BN = 64 * TN, WM = 32 * TM, WN = 32 * TN;
   constexpr bool IM = (BLD == B_IM2COL || BLD == B_IMT2 || BLD == B_IM1X1 || BLD == B_IMTAB || BLD == B_IMTAP ||
                        BLD == B_IM1X1S);
   constexpr bool SOFF = (BLD == B_IMTAP || BLD == B_IM1X1S);  // rows differ by a scalar soffset only
@@ -385,23 +387,25 @@ __global__ __launch_bounds__(256) void ring_kernel(GemmArgs p) {
         v[j] = (p.relu && x < 0.0f) ? 0.0f : x;
       }
       if constexpr (IM) {
-        float *const crow = p.c + (size_t)m * p.OHW;
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          if (cofs[j] >= 0) crow[cofs[j]] = v[j];
+          if (cofs[j] >= 0) out_elem1(p, (size_t)m * p.OHW + cofs[j], v[j]);
       } else {
-        float *const crow = p.c + (size_t)m * p.ldc + n_base;
-        if (p.cvec && n_base + TN <= p.N) {
+        const size_t crow = (size_t)m * p.ldc + n_base;
+        if (p.cvec && n_base + TN <= p.N && TN == 4) {
+          out_elem4(p, crow, f32x4v{v[0], v[TN > 1 ? 1 : 0], v[TN > 2 ? 2 : 0], v[TN > 3 ? 3 : 0]});
+        } else if (p.cvec && n_base + TN <= p.N && !p.wt) {
+          float *const cr = p.c + crow;
           typename fvec<TN>::t w;
           if constexpr (TN == 1) w = v[0]; else {
 #pragma unroll
             for (int j = 0; j < TN; ++j) w[j] = v[j];
           }
-          *(typename fvec<TN>::t *)crow = w;
+          *(typename fvec<TN>::t *)cr = w;
         } else {
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            if (n_base + j < p.N) crow[j] = v[j];
+            if (n_base + j < p.N) out_elem1(p, crow + j, v[j]);
         }
       }
     }
@@ -871,6 +875,15 @@ cfg_t ring_sgemm_cfg(const char *name) {
   c.k[A_KSCALAR][B_KSCALAR][0] = ring_kernel<TM, TN, BK, D, B_KSCALAR, 0>;  // (experiment: dword B, 16-B A)
   return c;
 }
+// 8 waves (4 x 2): 256-row tiles, two waves per SIMD on one stage
+template <int TM, int TN, int BK, int D>
+cfg_t ring_sgemm8_cfg(const char *name) {
+  cfg_t c{name, 128 * TM, 64 * TN, BK, 512, {}, 0};
+  c.k[A_KVEC][B_KVEC][0] = ring_kernel<TM, TN, BK, D, B_KVEC, 0, 4>;
+  c.k[A_KVEC][B_KVEC][1] = ring_kernel<TM, TN, BK, D, B_KVEC, 1, 4>;
+  c.k[A_KVEC][B_KVEC][2] = ring_kernel<TM, TN, BK, D, B_KVEC, 2, 4>;
+  return c;
+}
 
 }  // namespace
 
@@ -881,6 +894,9 @@ std::vector<cfg_t> ring_cfgs(int op) {
         ring_sgemm_cfg<2, 2, 64, 2>("r128x128x64d2"),
         ring_sgemm_cfg<2, 2, 32, 2>("r128x128x32d2"),
         ring_sgemm_cfg<2, 4, 32, 3>("r128x256x32d3"),
+        ring_sgemm8_cfg<2, 2, 32, 2>("r256x128x32d2w8"),
+        ring_sgemm8_cfg<2, 2, 16, 3>("r256x128x16d3w8"),
+        ring_sgemm8_cfg<2, 2, 16, 4>("r256x128x16d4w8"),
         srk_sgemm_cfg<2, 2, 32, 2>("srk128x128x32d2"),
         srk_sgemm_cfg<2, 2, 16, 4>("srk128x128x16d4"),
         srk_sgemm_cfg<2, 2, 32, 4>("srk128x128x32d4"),
