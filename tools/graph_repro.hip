@@ -1,5 +1,5 @@
 // graph_repro.hip -- minimal hipGraph replay, for the rocprofv3 kernel-trace crash inside
-// hipGraphLaunch (tools/job_r02_prof.sh): one trivial kernel captured from a non-blocking
+// hipGraphLaunch (tools/job_final.sh, step profgraph): one trivial kernel captured from a non-blocking
 // stream and replayed, nothing of libboda_hip. Diagnostic only.
 //   hipcc --offload-arch=gfx950 -O2 -o tools/graph_repro tools/graph_repro.hip
 //   rocprofv3 --kernel-trace --stats -d out -o t -- tools/graph_repro [nodes] [big-args 0/1] [cycles] [replays]
