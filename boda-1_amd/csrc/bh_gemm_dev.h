@@ -380,6 +380,17 @@ int launch_dcm(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
 std::vector<cfg_t> k1s_cfgs();
 int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
                uint32_t sx, uint32_t splits, bool first);
+// bh_wino.hip: Winograd F(2x2, 3x3) configurations for stride-1 3x3 convs; u = the Winograd bank
+// (the part of a 3x3 pack behind the k-major bank)
+std::vector<cfg_t> wg_cfgs();
+int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
+              float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+              uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
+              bool first);
+size_t wino_bank_floats(uint32_t OC, uint32_t IC);
+int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, bool first, bool last);
+// floats of the k-major bank (the first part of every pack)
+size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 // split-K / stream-K workspace and arrival tickets of the context (bh_gemm.hip)
 int ensure_ws(bh_ctx *ctx, size_t bytes);
 int ensure_cnt(bh_ctx *ctx, uint64_t n);

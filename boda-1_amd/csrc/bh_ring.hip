@@ -949,6 +949,10 @@ int launch_xpose_filts(bh_ctx *ctx, const float *w, float *wp, uint32_t OC, uint
                     last, "xpose_filts");
 }
 
+size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
+  return (size_t)(((uint64_t)IC * KY * KX + 63) & ~63ull) * ((OC + 3) & ~3u);
+}
+
 int ensure_wpack(bh_ctx *ctx, size_t bytes) {
   return bh::grow_buffer(ctx, ctx->wpack, ctx->wpack_bytes, bytes, false, "filter-bank pack buffer");
 }
@@ -956,12 +960,17 @@ int ensure_wpack(bh_ctx *ctx, size_t bytes) {
 }  // namespace bhk
 
 namespace bh {
+// the k-major bank, then for 3x3 kernels the Winograd bank U (bh_wino.hip) right behind it
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
-  return (size_t)(((uint64_t)IC * KY * KX + 63) & ~63ull) * ((OC + 3) & ~3u);
+  return bhk::kmajor_floats(OC, IC, KY, KX) + (KY == 3 && KX == 3 ? bhk::wino_bank_floats(OC, IC) : 0);
 }
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX) {
   if (conv_filts_packed_floats(OC, IC, KY, KX) * 4 >= 0x7fffffc0ull) return fail(BH_UNSUP, "conv_filts_pack: bank larger than 2 GiB");
-  return bhk::launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, true, true);  // a call of its own
+  const bool w3 = KY == 3 && KX == 3;
+  int rc = bhk::launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, true, !w3);  // a call of its own
+  if (rc == BH_OK && w3)
+    rc = bhk::launch_wino_pack(ctx, filts, packed + bhk::kmajor_floats(OC, IC, KY, KX), OC, IC, false, true);
+  return rc;
 }
 }  // namespace bh

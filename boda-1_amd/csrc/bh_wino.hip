@@ -1,0 +1,581 @@
+// bh_wino.hip -- Winograd F(2x2, 3x3) convolution for stride-1 3x3 convs (pad 0 or 1).
+//
+// The conv set's 3x3 stride-1 layers (GoogLeNet 3x3 branches, AlexNet conv3-5, NiN, VGG, the
+// ResNet bottleneck 3x3) are most of its MFMA-bound time (BASELINE.md §1.2 model: 2*M*N*K with
+// K = IC*9). F(2x2, 3x3) computes each 2x2 output tile from a 4x4 input patch with 16
+// elementwise products per (input, output) channel pair instead of 36: 2.25x fewer MFMA flops.
+// Boda itself reaches this algorithm through its cudnn_conv comparator (src/rtc_prof.cc:314-319
+// widens the compare tolerance for cuDNN's 3x3 Winograd); here it is a variant of the
+// conv op like the reference's tconv / k1conv choices (src/cnn_op.cc:16-331), routed per shape
+// by the tuning table only where it is faster, and checked against the direct-accumulation
+// oracle at the same tolerances as every other route.
+//
+//   U = G g G^T (filters, 4x4 per (oc, ic)), V = B^T d B (input patch), M = sum_ic U . V,
+//   Y = A^T M A (2x2 outputs), with
+//   G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1], B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1],
+//   A^T = [1 1 1 0; 0 1 -1 -1].
+//
+// MI355X structure (one fused kernel: nothing of U, V or M goes to HBM):
+//  * the filter transform is part of the filter-bank pack (bh_conv_filts_pack, Boda's
+//    xpose_filts role: once per net / op list, untimed as in the reference, src/rtc_prof.cc:93-99):
+//    U [IC4][OC32][16], each (ic, oc) row's four 4-float chunks rotated by (oc >> 2) & 3 so that
+//    16 lanes reading 16 consecutive output channels' chunk x with ds_read_b128 hit 16 distinct
+//    4-bank groups (conflict-free, MI355X_MICROARCH.md §LDS);
+//  * a block owns OCT = 32*NWO output channels x TT = 32*NWT Winograd tiles of the flattened
+//    (image, tile row, tile column) space; a stage is WCI = 4 input channels: the U slice
+//    [4][OCT][16] (16-B LDS-DMA) and the input strip [4][RIN][WPM] -- the "virtual" padded rows
+//    the tiles' patches touch (img*VH + iy + py, rows outside an image read as zero) at a pitch
+//    WPM > W whose zero tail also serves a patch's left neighbour (the previous row's tail);
+//  * per stage the block transforms the next stage's strip into V [4][TT][16] (one (channel,
+//    tile) pair per thread: 16 LDS reads, 32 adds, four ds_write_b128 at the same rotation), so
+//    each (tile, channel) is transformed once per block and shared by its NWO channel waves;
+//  * a wave owns 32 channels x 32 tiles x all 16 Winograd positions: v_mfma_f32_16x16x4_f32
+//    (exact fp32) with k = the stage's 4 channels, A = U (rows: channels), B = V (columns:
+//    tiles): 2 x 2 x 16 accumulator tiles (256 AGPRs, one wave per SIMD), 64 MFMAs per stage;
+//    every lane then holds all 16 positions of its (channel, tile) pairs, so the output
+//    transform, bias, residual and ReLU run in registers;
+//  * a persistent stream-K grid deals the (tile, stage) iterations equally between blocks (as
+//    bh_dcm.hip); a tile cut between blocks is summed after the output transform (linear) by
+//    its last-arriving block in block order: bitwise reproducible.
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+
+struct WgArgs {
+  const float *u;    // Winograd bank [IC4][OC32][16] (rotated chunks)
+  const float *in;   // B x IC x H x W
+  float *out;        // image stride OCOHW (channel slabs)
+  const float *bias; // OC or null
+  const float *res;  // laid out like out, or null
+  float *ws;         // stream-K slabs, two per block
+  uint32_t *cnt;     // arrival tickets, one per tile
+  uint32_t u_bytes, in_bytes, out_bytes;
+  uint32_t OC, OC32, IC, B, H, W, py, px, OH, OW, OHW, HW, ICHW, OCOHW;
+  uint32_t TW, TPI, VH, T;   // tiles per tile row / per image, virtual rows per image, tiles in all
+  uint32_t WPM, RW;          // strip pitch, RIN * WPM
+  uint32_t tw_m, tw_s, tpi_m, tpi_s, vh_m, vh_s, wpm_m, wpm_s, rw_m, rw_s;
+  uint32_t tiles_m, tm_m, tm_s;  // output-channel tiles (+ fastdiv)
+  uint32_t ipt, ipt_m, ipt_s, ipb, total_it;
+  int relu, wt;
+#ifdef BH_KTRACE
+  unsigned long long *trace;
+#endif
+};
+
+namespace {
+
+constexpr int WCI = 4;  // input channels per stage (the k of one 16x16x4 MFMA)
+
+// Filter transform: u[ic][oc][chunk rotated] = G g G^T for oc < OC32, ic < IC4 (zero past OC / IC)
+__global__ __launch_bounds__(256) void wino_pack_kernel(const float *__restrict__ w, float *__restrict__ u,
+                                                        uint32_t OC, uint32_t IC, uint32_t OC32, uint32_t IC4) {
+  const uint32_t e = blockIdx.x * 256u + threadIdx.x;  // ic * OC32 + oc
+  if (e >= IC4 * OC32) return;
+  const uint32_t ic = e / OC32, oc = e - ic * OC32;
+  float g[3][3];
+  const bool ok = oc < OC && ic < IC;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g[r][c] = ok ? w[((size_t)oc * IC + ic) * 9 + r * 3 + c] : 0.0f;
+  float t[4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    t[0][c] = g[0][c];
+    t[1][c] = 0.5f * (g[0][c] + g[1][c] + g[2][c]);
+    t[2][c] = 0.5f * (g[0][c] - g[1][c] + g[2][c]);
+    t[3][c] = g[2][c];
+  }
+  float *const dst = u + (size_t)e * 16;
+  const uint32_t rot = (oc >> 2) & 3u;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const f32x4v v = {t[x][0], 0.5f * (t[x][0] + t[x][1] + t[x][2]), 0.5f * (t[x][0] - t[x][1] + t[x][2]), t[x][2]};
+    *(f32x4v *)(dst + ((x + rot) & 3u) * 4) = v;
+  }
+}
+
+// logical block of hardware block bid: blocks b, b+8, ... share an XCD under round-robin
+// placement, so each XCD gets a contiguous run of iterations (neighbouring tiles in its L2)
+__device__ __forceinline__ uint32_t wg_lb(uint32_t bid, uint32_t G) {
+  const uint32_t xcd = bid & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void wg_store1(const WgArgs &p, __amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_SC1);
+  else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_OUT);
+}
+
+// NWO x NWT waves (32 channels x 32 tiles each); D-slot DMA ring (D >= 3); V4: 16-B strip pieces
+// (W % 4 == 0); SP: strip DMA pieces per thread and stage (the slot's strip capacity)
+template <int NWO, int NWT, int D, int V4, int SP>
+__global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
+  constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT;
+  constexpr int UF = WCI * OCT * 16;          // U floats per slot
+  static_assert(UF % (4 * NT) == 0, "whole U pieces per thread");
+  constexpr int LWU = UF / (4 * NT);          // 16-B U pieces per thread and stage
+  constexpr int PW = V4 ? 4 : 1;              // floats per strip piece
+  constexpr int SCAP = SP * NT * PW;          // strip floats per slot
+  constexpr int GZ = 4;                       // zero guard before the strip (a patch's left neighbour of row 0)
+  constexpr int SLOT = UF + GZ + SCAP;
+  constexpr int VSZ = WCI * TT * 16;          // floats of one V buffer
+  constexpr int LW = LWU + SP;
+  constexpr int NQ = 16;                      // float4 results per lane: (a, b, j)
+  static_assert(D >= 3 && (D - 3) * LW <= 63, "vmcnt range");
+  static_assert(WCI * TT <= NT, "one transform pair per thread");
+  static_assert((SLOT % 4) == 0 && (UF + GZ) % 4 == 0, "16-B aligned slot parts");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *const vbase = smem + D * SLOT;
+  uint32_t *const flag = (uint32_t *)(vbase + 2 * VSZ);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave % NWO, wtl = wave / NWO;
+  const int li = lane & 15, lg = lane >> 4;
+  const uint32_t lb = wg_lb(blockIdx.x, gridDim.x);
+  const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
+  if (tid < D * GZ) smem[(tid / GZ) * SLOT + UF + tid % GZ] = 0.0f;
+#ifdef BH_KTRACE
+  if (threadIdx.x == 0) p.trace[(size_t)blockIdx.x * 8 + 0] = wall_clock64();
+#endif
+
+  // tile t = (tile group, OC tile), OC tile fastest (consecutive tiles share the strip via L2)
+  auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &g0) {
+    const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
+    oc0 = (t - pt * p.tiles_m) * OCT;
+    g0 = pt * TT;
+  };
+  // Winograd tile tg: virtual strip row of its patch's top, its patch's first input column
+  auto tpos = [&](uint32_t tg, uint32_t &v, int &x) {
+    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    v = img * p.VH + 2 * ty;
+    x = 2 * (int)tx - (int)p.px;
+  };
+
+  // ---- DMA sources: tile-independent per-lane parts
+  const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
+  uint32_t urel[LWU];
+#pragma unroll
+  for (int j = 0; j < LWU; ++j) {  // piece e of the [4][OCT][16] slice: channel c, floats 4r .. of its OCT*16 run
+    const uint32_t e = (uint32_t)((j * NW + wave) * 64 + lane), c = e / (4 * OCT), r = e % (4 * OCT);
+    urel[j] = (c * p.OC32 * 16 + r * 4) * 4;
+  }
+  uint32_t uvo[LWU], svo[SP];
+  uint32_t ls_tile = 0xffffffffu;
+  // scalar parts of iteration it (tile it / ipt, channel group it % ipt); true: a dead stage
+  auto plan = [&](uint32_t it, uint32_t &su, uint32_t &ss) -> bool {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * WCI;
+    if (t != ls_tile) {  // uniform
+      uint32_t oc0, g0;
+      tile_of(t, oc0, g0);
+#pragma unroll
+      for (int j = 0; j < LWU; ++j) uvo[j] = urel[j] + oc0 * 64u;
+      uint32_t v0;
+      int x0;
+      tpos(g0 < p.T ? g0 : 0u, v0, x0);
+#pragma unroll
+      for (int j = 0; j < SP; ++j) {  // strip piece: channel c, row s, column col of the [4][RIN][WPM] image
+        const uint32_t f = (uint32_t)((j * NW + wave) * 64 + lane) * PW;
+        const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
+        const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
+        const uint32_t v = v0 + s;
+        const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
+        const uint32_t iy = v - img * p.VH - p.py;  // wraps (misses) in the top padding
+        const bool ok = (c < (uint32_t)WCI) & (col < p.W) & (iy < p.H) & (img < p.B);
+        svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + col) * 4u);
+      }
+      ls_tile = t;
+    }
+    su = ic0 * p.OC32 * 64u;
+    ss = ic0 * p.HW * 4u;
+    return it >= it1;
+  };
+  auto issue_one = [&](int q, int slot, uint32_t su, uint32_t ss, bool dead) {
+    float *const base = smem + slot * SLOT;
+    if (q < LWU) {
+      dma16s(dead ? rnull : rsu, base + (q * NW + wave) * 256, uvo[q], su);
+    } else {
+      const int j = q - LWU;
+      if constexpr (V4) dma16s(dead ? rnull : rsi, base + UF + GZ + (j * NW + wave) * 256, svo[j], ss);
+      else dma4s(dead ? rnull : rsi, base + UF + GZ + (j * NW + wave) * 64, svo[j], ss);
+    }
+  };
+
+  // ---- input transform: thread (cl, tt) of the first 4*TT, the patch of tile g0 + tt, channel cl
+  const uint32_t xcl = (uint32_t)tid / TT, xtt = (uint32_t)tid % TT;
+  uint32_t xb = GZ;  // the patch's first float in the strip (guard included)
+  uint32_t lx_tile = 0xffffffffu;
+  auto xplan = [&](uint32_t it) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    if (t == lx_tile) return;
+    lx_tile = t;
+    uint32_t oc0, g0;
+    tile_of(t, oc0, g0);
+    uint32_t v0;
+    int x0;
+    tpos(g0 < p.T ? g0 : 0u, v0, x0);
+    const uint32_t tg = g0 + xtt;
+    xb = GZ;
+    if (tg < p.T) {
+      uint32_t v;
+      int x;
+      tpos(tg, v, x);
+      xb = (uint32_t)((int)(GZ + xcl * p.RW + (v - v0) * p.WPM) + x);
+    }
+  };
+  auto transform = [&](int sl, int vb) {
+    if (tid < WCI * TT) {
+      const float *const s = smem + sl * SLOT + UF + xb;
+      const uint32_t wpm = p.WPM;
+      float d[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[r][c] = s[r * wpm + c];
+      float t[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t[0][c] = d[0][c] - d[2][c];
+        t[1][c] = d[1][c] + d[2][c];
+        t[2][c] = d[2][c] - d[1][c];
+        t[3][c] = d[1][c] - d[3][c];
+      }
+      float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
+      const uint32_t rot = (xtt >> 2) & 3u;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const f32x4v v = {t[x][0] - t[x][2], t[x][1] + t[x][2], t[x][2] - t[x][1], t[x][1] - t[x][3]};
+        *(f32x4v *)(vd + ((x + rot) & 3u) * 4) = v;
+      }
+    }
+  };
+
+  // ---- MFMA stage: lane (li, lg): channel k = lg of the stage; A row = output channel
+  // oc0 + wo*32 + 16a + li, B column = tile wtl*32 + 16b + li; chunk x of its 16 positions sits at
+  // ((x + rot) & 3) * 4 (the same rotation for U and V: (li >> 2) & 3)
+  f32x4v acc[2][2][16];
+  const uint32_t rot = ((uint32_t)li >> 2) & 3u;
+  uint32_t co[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) co[x] = ((x + rot) & 3u) * 4u;
+  // the stage's 16 fragment reads go out together (one LDS round trip), then the MFMAs in x order
+  // (x's group waits only for its own reads); hipcc otherwise issues each read just before its
+  // MFMAs and waits on every one
+  f32x4v uf[2][4], vf[2][4];
+  auto frags = [&](int sl, int vb) {
+    const float *const ub = smem + sl * SLOT + (lg * OCT + wo * 32 + li) * 16;
+    const float *const vp = vbase + vb * VSZ + (lg * TT + wtl * 32 + li) * 16;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        uf[a][x] = *(const f32x4v *)(ub + a * 256 + co[x]);
+        vf[a][x] = *(const f32x4v *)(vp + a * 256 + co[x]);
+      }
+  };
+  auto mfmas = [&]() {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+
+  // output transform of accumulator group q = (a*2 + b)*4 + j: {y00, y01, y10, y11} of output
+  // channel oc0 + wo*32 + 16a + 4lg + j, tile wtl*32 + 16b + li
+  auto out_q = [&](int q) -> f32x4v {
+    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
+    float s0[4], s1[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      // explicit AGPR reads at this point: hipcc otherwise copies all 256 accumulators to VGPRs at
+      // the loop exit, and the epilogue spills
+      float m0, m1, m2, m3;
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m0) : "a"(acc[a][b][n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m1) : "a"(acc[a][b][4 + n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m2) : "a"(acc[a][b][8 + n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m3) : "a"(acc[a][b][12 + n][j]));
+      s0[n] = m0 + m1 + m2;
+      s1[n] = m1 - m2 - m3;
+    }
+    return f32x4v{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]};
+  };
+  // bias (prefetched per tile), residual, ReLU and masked stores of group q's results
+  float bias[2][4];
+  auto store_q = [&](uint32_t oc0, uint32_t g0, int q, f32x4v yy) {
+    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
+    const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
+    const bool tv = tg < p.T;
+    const uint32_t tgc = tv ? tg : 0u;
+    const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    const uint32_t oy = 2 * ty, ox = 2 * tx;
+    const bool x1 = ox + 1 < p.OW, y1 = oy + 1 < p.OH;
+    const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
+    const bool ok = tv & (oc < p.OC);
+    const uint32_t o = img * p.OCOHW + oc * p.OHW + oy * p.OW + ox;
+    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & x1, (o + 1) * 4u),
+                             oob_unless(ok & y1, (o + p.OW) * 4u), oob_unless(ok & x1 & y1, (o + p.OW + 1) * 4u)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float z = yy[e] + bias[a][j];
+      if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
+      z = (p.relu && z < 0.0f) ? 0.0f : z;
+      wg_store1(p, rso, off[e], z);
+    }
+  };
+  // tile t done in this block: store it, or hand the partial tile over through this block's slab
+  // and the tile's ticket (the last arriver sums the slabs in block order)
+  auto finish_tile = [&](uint32_t t) {
+    uint32_t oc0, g0;
+    tile_of(t, oc0, g0);
+    const uint32_t tb = t * p.ipt;
+    const bool whole = tb >= it0 && tb + p.ipt <= it1;  // uniform
+    const uint32_t sl = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (NQ * NT * 4), NQ * NT * 16);
+    // one group at a time: its 16 accumulators out of the AGPRs, transformed, stored (whole tile)
+    // or written to the slab (hipcc otherwise reads all 256 AGPRs before the branch and spills)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const f32x4v y = out_q(q);
+      if (whole)
+        store_q(oc0, g0, q, y);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y), rw,
+                                               (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (whole) return;
+    const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == b1 - b0 ? 1u : 0u;
+      if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+    const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+    // four result groups at a time, every block's slab of them in flight, summed in block order
+    // (block order = k order: bitwise reproducible)
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += 4) {
+      f32x4v y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      for (uint32_t b = b0; b <= b1; ++b) {
+        const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+        const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
+        f32x4v x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          x[i] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rall, base + (uint32_t)(((q0 + i) * NT + tid) * 16), 0, AUX_SC1));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] += x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) store_q(oc0, g0, q0 + i, y[i]);
+    }
+  };
+
+  // ---- prologue: stages it0 .. it0+D-2 in flight; the first stage's strip transformed
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) {
+    uint32_t su, ss;
+    const bool dead = plan(it0 + (uint32_t)s, su, ss);
+#pragma unroll
+    for (int q = 0; q < LW; ++q) issue_one(q, s, su, ss, dead);
+  }
+  vm_wait<(D - 2) * LW>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // stage it0 landed for every wave (and the guards are written)
+  asm volatile("" ::: "memory");
+  xplan(it0);
+  transform(0, 0);
+  int slot = 0, vb = 0;
+  uint32_t it = it0;
+  while (it < it1) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    const uint32_t iend = min(it1, (t + 1) * p.ipt);
+    {
+      uint32_t oc0, g0;
+      tile_of(t, oc0, g0);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
+          bias[a][j] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[a][b][q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    for (; it < iend; ++it) {
+      vm_wait<(D - 3) * LW>();  // stage it+1 landed (this wave's DMAs)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // ... every wave's; V(it) written; slot of it-1 and V(it+1)'s buffer free
+      asm volatile("" ::: "memory");
+      {
+        uint32_t su, ss;
+        const bool dead = plan(it + D - 1, su, ss);
+        const int islot = slot == 0 ? D - 1 : slot - 1;
+#pragma unroll
+        for (int q = 0; q < LW; ++q) issue_one(q, islot, su, ss, dead);
+      }
+      frags(slot, vb);
+      __builtin_amdgcn_sched_barrier(0);
+      xplan(it + 1);
+      transform(slot == D - 1 ? 0 : slot + 1, vb ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas();
+      slot = slot == D - 1 ? 0 : slot + 1;
+      vb ^= 1;
+    }
+    finish_tile(t);
+  }
+  vm_wait<0>();
+}
+
+template <int NWO, int NWT, int D, int V4, int SP>
+cfg_t wg_cfg(const char *name) {
+  cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wg_kernel<NWO, NWT, D, V4, SP>;
+  c.dc = 4;
+  c.dc_ky = 3;
+  c.dc_kx = 3;
+  c.dc_s = V4;
+  c.dc_rin = SP;
+  c.dc_ci = D;
+  return c;
+}
+
+}  // namespace
+
+std::vector<cfg_t> wg_cfgs() {
+  // <NWO, NWT, D, V4, SP>: OCT = 32 NWO channels x TT = 32 NWT tiles; SP strip pieces per thread
+  return {
+      wg_cfg<2, 2, 3, 1, 4>("wg64x64v"), wg_cfg<2, 2, 3, 0, 8>("wg64x64"),
+      wg_cfg<2, 2, 4, 1, 3>("wg64x64vd4"), wg_cfg<2, 2, 4, 0, 6>("wg64x64d4"),
+      wg_cfg<4, 1, 3, 1, 2>("wg128x32v"), wg_cfg<4, 1, 3, 0, 6>("wg128x32"),
+  };
+}
+
+size_t wino_bank_floats(uint32_t OC, uint32_t IC) {
+  return (size_t)((IC + 3) & ~3u) * ((OC + 31) & ~31u) * 16;
+}
+
+int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, bool first, bool last) {
+  uint32_t OC32 = (OC + 31) & ~31u, IC4 = (IC + 3) & ~3u;
+  const uint64_t n = (uint64_t)OC32 * IC4;
+  void *args[] = {(void *)&filts, (void *)&u, (void *)&OC, (void *)&IC, (void *)&OC32, (void *)&IC4};
+  return bh::launch(ctx, (const void *)wino_pack_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), args, first, last,
+                    "wino_pack");
+}
+
+// Launch a Winograd configuration: UNSUP unless a stride-1 3x3 conv with pad <= 1, IC % 4 == 0,
+// whose strips fit the configuration's slot. splits: 0 / 1..4 blocks per CU, iterations dealt
+// equally; 5..8: blocks per CU 1..4, whole tiles per block.
+int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
+              float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+              uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
+              bool first) {
+  if (KY != 3 || KX != 3 || sy != 1 || sx != 1 || py > 1 || px > 1)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for stride-1 3x3 convs with pad <= 1");
+  if (IC % WCI) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs IC % 4 == 0");
+  if (c.dc_s && W % 4) return bh::fail(BH_UNSUP, std::string("conv: 16-B strip pieces of ") + c.name + " need W % 4 == 0");
+  WgArgs p{};
+  const uint32_t OH = H + 2 * py - 2, OW = W + 2 * px - 2;
+  const uint32_t TH = (OH + 1) / 2, TW = (OW + 1) / 2, TPI = TH * TW;
+  const uint64_t T64 = (uint64_t)B * TPI;
+  const uint32_t OCT = (uint32_t)c.BM, TT = (uint32_t)c.BN, NT = (uint32_t)c.NT, D = (uint32_t)c.dc_ci;
+  const uint32_t VH = std::max(H + 2 * py, 2 * TH + 2);
+  const uint32_t WPM = (std::max(W + 1, 2 * TW + 2 - px) + 3) & ~3u;
+  if (T64 >= (1u << 30) || (uint64_t)B * VH >= (1u << 30)) return bh::fail(BH_UNSUP, "conv: too many Winograd tiles");
+  const uint32_t T = (uint32_t)T64, ngroups = (T + TT - 1) / TT;
+  auto vrow = [&](uint32_t tg) { return (tg / TPI) * VH + 2 * ((tg % TPI) / TW); };
+  uint32_t rin = 0;
+  for (uint32_t gi = 0; gi < ngroups; ++gi) {
+    const uint32_t a = gi * TT, b = std::min(T, a + TT) - 1;
+    rin = std::max(rin, vrow(b) + 4 - vrow(a));
+  }
+  const uint32_t PW = c.dc_s ? 4 : 1, SP = (uint32_t)c.dc_rin;
+  if ((uint64_t)WCI * rin * WPM > (uint64_t)SP * NT * PW)
+    return bh::fail(BH_UNSUP, std::string("conv: input strip too large for ") + c.name);
+  const uint64_t out_bytes = (uint64_t)B * out_ctot * OH * OW * 4;
+  if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the Winograd kernel");
+  const uint32_t OC32 = (OC + 31) & ~31u;
+  p.u = u; p.in = in; p.out = out; p.bias = bias; p.res = res;
+  p.u_bytes = (uint32_t)(wino_bank_floats(OC, IC) * 4);
+  p.in_bytes = (uint32_t)((uint64_t)B * IC * H * W * 4);
+  p.out_bytes = (uint32_t)out_bytes;
+  p.OC = OC; p.OC32 = OC32; p.IC = IC; p.B = B; p.H = H; p.W = W; p.py = py; p.px = px;
+  p.OH = OH; p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = out_ctot * OH * OW;
+  p.TW = TW; p.TPI = TPI; p.VH = VH; p.T = T; p.WPM = WPM; p.RW = rin * WPM;
+  bh::fastdiv f = bh::make_fastdiv(TW); p.tw_m = f.m; p.tw_s = f.s;
+  f = bh::make_fastdiv(TPI); p.tpi_m = f.m; p.tpi_s = f.s;
+  f = bh::make_fastdiv(VH); p.vh_m = f.m; p.vh_s = f.s;
+  f = bh::make_fastdiv(WPM); p.wpm_m = f.m; p.wpm_s = f.s;
+  f = bh::make_fastdiv(p.RW); p.rw_m = f.m; p.rw_s = f.s;
+  const uint32_t octiles = (OC + OCT - 1) / OCT, ipt = IC / WCI;
+  const uint64_t ntile = (uint64_t)ngroups * octiles, total = ntile * ipt;
+  if (total >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many iterations");
+  p.tiles_m = octiles;
+  f = bh::make_fastdiv(octiles); p.tm_m = f.m; p.tm_s = f.s;
+  p.ipt = ipt;
+  f = bh::make_fastdiv(ipt); p.ipt_m = f.m; p.ipt_s = f.s;
+  p.relu = relu;
+  p.wt = wt;
+  // dynamic LDS: D slots (U + guard + strip), two V buffers, the ticket flag
+  const uint32_t slot = WCI * OCT * 16 + 4 + SP * NT * PW;
+  const uint32_t lds = (D * slot + 2 * WCI * TT * 16 + 4) * 4;
+  if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: LDS too small for ") + c.name);
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+  const bool whole = splits > 4;
+  uint32_t bpc = splits ? (whole ? splits - 4 : splits) : 1;
+  bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  uint64_t G = (uint64_t)ncu * bpc;
+  uint32_t ipb = (uint32_t)((total + G - 1) / G);
+  if (whole) ipb = (uint32_t)((ntile + G - 1) / G) * ipt;
+  G = (total + ipb - 1) / ipb;
+  p.ipb = ipb;
+  p.total_it = (uint32_t)total;
+  int rc = ensure_ws(ctx, (size_t)2 * G * NT * 16 * 16);  // two slabs of 16 float4 per thread per block
+  if (rc == BH_OK) rc = ensure_cnt(ctx, (size_t)ntile);
+  if (rc != BH_OK) return rc;
+  p.ws = (float *)ctx->ws;
+  p.cnt = (uint32_t *)ctx->cnt;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(NT), args, first, true, "conv_wino", lds);
+}
+
+}  // namespace bhk

@@ -41,7 +41,7 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
-    if name.startswith(("dc", "dm", "fcv", "ks")):
+    if name.startswith(("dc", "dm", "fcv", "ks", "wg")):
         return 1 << 30
     if name.startswith("gv"):
         m = re.search(r"w(\d+)", name)
@@ -163,6 +163,10 @@ def main():
                     if cn.startswith("dc"):  # direct conv (stems): no K split; UNSUP for other kernels
                         if kind == 1 and cn.startswith("dc%ds%d" % (s.KY, s.sy)) and s.KX == s.KY and s.sx == s.sy:
                             cand.append((ci, 0))
+                        continue
+                    if cn.startswith("wg"):  # Winograd 3x3: S = grid mode as stream-K; UNSUP for other ops
+                        if kind == 1 and s.KY == s.KX == 3 and s.sy == s.sx == 1 and s.py <= 1 and s.px <= 1:
+                            cand += [(ci, 1), (ci, 2), (ci, 5)]
                         continue
                     if cn.startswith("ks"):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 1 and s.sy == s.sx == 1 and s.py == s.px == 0:
