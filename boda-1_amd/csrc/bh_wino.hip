@@ -37,6 +37,8 @@
 //  * a persistent stream-K grid deals the (tile, stage) iterations equally between blocks (as
 //    bh_dcm.hip); a tile cut between blocks is summed after the output transform (linear) by
 //    its last-arriving block in block order: bitwise reproducible.
+#include <type_traits>
+
 #include "bh_gemm_dev.h"
 
 namespace bhk {
@@ -55,6 +57,8 @@ struct WgArgs {
   uint32_t WPM, RW;          // strip pitch, RIN * WPM
   uint32_t tw_m, tw_s, tpi_m, tpi_s, vh_m, vh_s, wpm_m, wpm_s, rw_m, rw_s;
   uint32_t tiles_m, tm_m, tm_s;  // output-channel tiles (+ fastdiv)
+  uint32_t ngr, ngr_m, ngr_s;    // tile groups (+ fastdiv)
+  int ocs;                       // tile order: 0 = output-channel tile fastest, 1 = slowest
   uint32_t ipt, ipt_m, ipt_s, ipb, total_it;
   int relu, wt;
 #ifdef BH_KTRACE
@@ -109,7 +113,9 @@ __device__ __forceinline__ void wg_store1(const WgArgs &p, __amdgpu_buffer_rsrc_
 
 // NWO x NWT waves (32 channels x 32 tiles each); D-slot DMA ring (D >= 3); V4: 16-B strip pieces
 // (W % 4 == 0); SP: strip DMA pieces per thread and stage (the slot's strip capacity)
-template <int NWO, int NWT, int D, int V4, int SP>
+// DBG (diagnostic builds only; wrong results by design): bit 0 = no input transform in the loop,
+// bit 1 = no MFMA, bit 2 = no DMA after the prologue, bit 3 = no output stores
+template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
 __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
   constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT;
   constexpr int UF = WCI * OCT * 16;          // U floats per slot
@@ -136,15 +142,21 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
   const uint32_t lb = wg_lb(blockIdx.x, gridDim.x);
   const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
   if (tid < D * GZ) smem[(tid / GZ) * SLOT + UF + tid % GZ] = 0.0f;
-#ifdef BH_KTRACE
-  if (threadIdx.x == 0) p.trace[(size_t)blockIdx.x * 8 + 0] = wall_clock64();
-#endif
 
   // tile t = (tile group, OC tile), OC tile fastest (consecutive tiles share the strip via L2)
+  // tile t = (tile group, OC tile): OC tile fastest (consecutive tiles share the strip through L2),
+  // or slowest (ocs: an XCD's run of tiles shares one OC tile's U slice -- U outgrows the L2 where
+  // IC*OC is large)
   auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &g0) {
-    const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
-    oc0 = (t - pt * p.tiles_m) * OCT;
-    g0 = pt * TT;
+    if (p.ocs) {
+      const uint32_t q = fdiv(t, p.ngr_m, p.ngr_s);
+      oc0 = q * OCT;
+      g0 = (t - q * p.ngr) * TT;
+    } else {
+      const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
+      oc0 = (t - pt * p.tiles_m) * OCT;
+      g0 = pt * TT;
+    }
   };
   // Winograd tile tg: virtual strip row of its patch's top, its patch's first input column
   auto tpos = [&](uint32_t tg, uint32_t &v, int &x) {
@@ -227,15 +239,21 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
       xb = (uint32_t)((int)(GZ + xcl * p.RW + (v - v0) * p.WPM) + x);
     }
   };
-  auto transform = [&](int sl, int vb) {
+  // split in two so the reads go out with the stage's fragment reads and the adds sit between MFMA
+  // groups: the 4x4 patch into d, then B^T d B into V
+  float d[4][4];
+  auto tx_read = [&](int sl) {
     if (tid < WCI * TT) {
       const float *const s = smem + sl * SLOT + UF + xb;
       const uint32_t wpm = p.WPM;
-      float d[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) d[r][c] = s[r * wpm + c];
+    }
+  };
+  auto tx_write = [&](int vb) {
+    if (tid < WCI * TT) {
       float t[4][4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -252,6 +270,10 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
         *(f32x4v *)(vd + ((x + rot) & 3u) * 4) = v;
       }
     }
+  };
+  auto transform = [&](int sl, int vb) {
+    tx_read(sl);
+    tx_write(vb);
   };
 
   // ---- MFMA stage: lane (li, lg): channel k = lg of the stage; A row = output channel
@@ -277,18 +299,14 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
         vf[a][x] = *(const f32x4v *)(vp + a * 256 + co[x]);
       }
   };
-  auto mfmas = [&]() {
+  auto mfma_x = [&](int x) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-            acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int b = 0; b < 2; ++b)
+          acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
   };
 
   const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
@@ -316,26 +334,37 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
   };
   // bias (prefetched per tile), residual, ReLU and masked stores of group q's results
   float bias[2][4];
-  auto store_q = [&](uint32_t oc0, uint32_t g0, int q, f32x4v yy) {
+  // a tile's output positions, once per tile (b: column tile): image base + (2ty, 2tx) offset,
+  // and which of the 2x2 outputs exist (odd OH / OW, tiles past the op)
+  uint32_t sob[2];
+  bool stv[2], sx1[2], sy1[2];
+  auto store_pos = [&](uint32_t g0) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
+      stv[b] = tg < p.T;
+      const uint32_t tgc = stv[b] ? tg : 0u;
+      const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
+      const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+      sx1[b] = 2 * tx + 1 < p.OW;
+      sy1[b] = 2 * ty + 1 < p.OH;
+      sob[b] = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
+    }
+  };
+  auto store_q = [&](uint32_t oc0, int q, f32x4v yy) {
     const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
-    const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
-    const bool tv = tg < p.T;
-    const uint32_t tgc = tv ? tg : 0u;
-    const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
-    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
-    const uint32_t oy = 2 * ty, ox = 2 * tx;
-    const bool x1 = ox + 1 < p.OW, y1 = oy + 1 < p.OH;
     const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
-    const bool ok = tv & (oc < p.OC);
-    const uint32_t o = img * p.OCOHW + oc * p.OHW + oy * p.OW + ox;
-    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & x1, (o + 1) * 4u),
-                             oob_unless(ok & y1, (o + p.OW) * 4u), oob_unless(ok & x1 & y1, (o + p.OW + 1) * 4u)};
+    const bool ok = stv[b] & (oc < p.OC);
+    const uint32_t o = sob[b] + oc * p.OHW;
+    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1[b], (o + 1) * 4u),
+                             oob_unless(ok & sy1[b], (o + p.OW) * 4u),
+                             oob_unless(ok & sx1[b] & sy1[b], (o + p.OW + 1) * 4u)};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float z = yy[e] + bias[a][j];
       if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
       z = (p.relu && z < 0.0f) ? 0.0f : z;
-      wg_store1(p, rso, off[e], z);
+      wg_store1(p, rso, (DBG & 8) ? OOB : off[e], z);
     }
   };
   // tile t done in this block: store it, or hand the partial tile over through this block's slab
@@ -345,6 +374,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
     tile_of(t, oc0, g0);
     const uint32_t tb = t * p.ipt;
     const bool whole = tb >= it0 && tb + p.ipt <= it1;  // uniform
+    store_pos(g0);
     const uint32_t sl = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (NQ * NT * 4), NQ * NT * 16);
     // one group at a time: its 16 accumulators out of the AGPRs, transformed, stored (whole tile)
@@ -353,7 +383,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
     for (int q = 0; q < NQ; ++q) {
       const f32x4v y = out_q(q);
       if (whole)
-        store_q(oc0, g0, q, y);
+        store_q(oc0, q, y);
       else
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y), rw,
                                                (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
@@ -392,10 +422,28 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
         for (int i = 0; i < 4; ++i) y[i] += x[i];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) store_q(oc0, g0, q0 + i, y[i]);
+      for (int i = 0; i < 4; ++i) store_q(oc0, q0 + i, y[i]);
     }
   };
 
+#ifdef BH_KTRACE
+  // per-phase shader-clock sums (s_memtime; its lgkmcnt wait distorts LDS overlap a little):
+  // [0] 0, [1] wait + barrier, [2] DMA issue, [3] fragment reads + input transform, [4] MFMA issue,
+  // [5] tile epilogues, [6] iterations, [7] whole block
+  uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t tk0 = __builtin_amdgcn_s_memtime();
+  uint64_t tkp = tk0;
+#define TK(i)                                                   \
+  do {                                                          \
+    const uint64_t tn_ = __builtin_amdgcn_s_memtime();          \
+    tk[i] += tn_ - tkp;                                         \
+    tkp = tn_;                                                  \
+  } while (0)
+#else
+#define TK(i) \
+  do {        \
+  } while (0)
+#endif
   // ---- prologue: stages it0 .. it0+D-2 in flight; the first stage's strip transformed
 #pragma unroll
   for (int s = 0; s < D - 1; ++s) {
@@ -433,35 +481,527 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[a][b][q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
     for (; it < iend; ++it) {
+#ifdef BH_KTRACE
+      tkp = __builtin_amdgcn_s_memtime();
+      tk[6] += 1;
+#endif
       vm_wait<(D - 3) * LW>();  // stage it+1 landed (this wave's DMAs)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // ... every wave's; V(it) written; slot of it-1 and V(it+1)'s buffer free
       asm volatile("" ::: "memory");
-      {
-        uint32_t su, ss;
-        const bool dead = plan(it + D - 1, su, ss);
-        const int islot = slot == 0 ? D - 1 : slot - 1;
-#pragma unroll
-        for (int q = 0; q < LW; ++q) issue_one(q, islot, su, ss, dead);
+      TK(1);
+      // the next stage's patch reads, this stage's fragment reads, then four MFMA groups with the
+      // stage it+D-1 DMAs and the patch's transform between them (their issue and latency under
+      // the MFMAs)
+      const int nslot = slot == D - 1 ? 0 : slot + 1, islot = slot == 0 ? D - 1 : slot - 1;
+      if constexpr ((DBG & 1) == 0) {
+        xplan(it + 1);
+        tx_read(nslot);
       }
       frags(slot, vb);
+      uint32_t su = 0, ss = 0;
+      bool dead = true;
+      if constexpr ((DBG & 4) == 0) dead = plan(it + D - 1, su, ss);
       __builtin_amdgcn_sched_barrier(0);
-      xplan(it + 1);
-      transform(slot == D - 1 ? 0 : slot + 1, vb ^ 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas();
+      TK(2);
+      constexpr int QG = (LW + 3) / 4;  // DMA issues per MFMA group
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        if constexpr ((DBG & 2) == 0) mfma_x(x);
+        else acc[0][0][x] += uf[0][x] + vf[0][x] + uf[1][x] + vf[1][x];
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((DBG & 4) == 0) {
+#pragma unroll
+          for (int q = x * QG; q < (x + 1) * QG && q < LW; ++q) issue_one(q, islot, su, ss, dead);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (x == 0) {
+          if constexpr ((DBG & 1) == 0) tx_write(vb ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+          TK(3);
+        }
+      }
+      TK(4);
       slot = slot == D - 1 ? 0 : slot + 1;
       vb ^= 1;
     }
+#ifdef BH_KTRACE
+    tkp = __builtin_amdgcn_s_memtime();
+#endif
     finish_tile(t);
+    TK(5);
   }
   vm_wait<0>();
+#ifdef BH_KTRACE
+  tk[7] = __builtin_amdgcn_s_memtime() - tk0;
+  if (tid == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p.trace[(size_t)blockIdx.x * 8 + i] = tk[i];
+  }
+#endif
 }
 
-template <int NWO, int NWT, int D, int V4, int SP>
+// wgp_kernel: the same Winograd stage, software-pipelined so that nothing but the barrier sits
+// between one stage's MFMAs and the next (the phase timings of wg_kernel, tools/wg_phases.py: per
+// stage ~2000 MFMA cycles beside ~1000 of LDS-read latency after the barrier and ~700 of LDS-DMA
+// issue):
+//  * U goes straight from L2 into registers (16-B loads of the lane's own [4 channels][16] rows;
+//    group x of stage it+1 right after group x of stage it's MFMAs) -- no LDS slot, no DMA, no
+//    ds_read for it;
+//  * V is triple-buffered: stage it+2's patches are transformed during stage it, so stage it+1's V
+//    is complete at the top of stage it and its fragments load under stage it's MFMAs;
+//  * the strip ring (LDS-DMA) holds stages it+2 .. it+D+1: each strip has two stages to land.
+template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
+__global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
+  constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT;
+  constexpr int PW = 4;                       // floats per strip piece (16 B; rows of W % 4 != 0 run
+                                              // into the next row: masked in the transform, !V4)
+  constexpr int SCAP = SP * NT * PW;          // strip floats per slot
+  constexpr int GZ = 4;                       // zero guard before the strip (a patch's left neighbour of row 0)
+  constexpr int SLOT = GZ + SCAP;
+  constexpr int VSZ = WCI * TT * 16;          // floats of one V buffer
+  constexpr int NU = 8;                       // U loads per stage and lane
+  constexpr int NQ = 16;                      // float4 results per lane: (a, b, j)
+  constexpr int WTOP = (D - 2) * (SP + NU);  // younger than stage it+2's strip at the top
+  static_assert(D >= 3 && WTOP <= 63, "vmcnt range");
+  static_assert(WCI * TT <= NT, "one transform pair per thread");
+  static_assert(SLOT % 4 == 0, "16-B aligned slots");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *const vbase = smem + D * SLOT;
+  uint32_t *const flag = (uint32_t *)(vbase + 3 * VSZ);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave % NWO, wtl = wave / NWO;
+  const int li = lane & 15, lg = lane >> 4;
+  const uint32_t lb = wg_lb(blockIdx.x, gridDim.x);
+  const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
+  if (tid < D * GZ) smem[(tid / GZ) * SLOT + tid % GZ] = 0.0f;
+
+  // tile t = (tile group, OC tile): OC tile fastest (consecutive tiles share the strip through L2),
+  // or slowest (ocs: an XCD's run of tiles shares one OC tile's U slice -- U outgrows the L2 where
+  // IC*OC is large)
+  auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &g0) {
+    if (p.ocs) {
+      const uint32_t q = fdiv(t, p.ngr_m, p.ngr_s);
+      oc0 = q * OCT;
+      g0 = (t - q * p.ngr) * TT;
+    } else {
+      const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
+      oc0 = (t - pt * p.tiles_m) * OCT;
+      g0 = pt * TT;
+    }
+  };
+  auto tpos = [&](uint32_t tg, uint32_t &v, int &x) {
+    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    v = img * p.VH + 2 * ty;
+    x = 2 * (int)tx - (int)p.px;
+  };
+
+  const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
+  // lane (li, lg): chunk x of its 16 positions sits at ((x + rot) & 3) * 4 in U's and V's rows
+  const uint32_t rot = ((uint32_t)li >> 2) & 3u;
+  uint32_t co[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) co[x] = ((x + rot) & 3u) * 4u;
+
+  // ---- strip DMA of stage it (channels ic0 .. ic0 + 3 of tile it / ipt)
+  uint32_t svo[SP];
+  uint32_t ls_tile = 0xffffffffu;
+  auto plan_strip = [&](uint32_t it, uint32_t &ss) -> bool {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * WCI;
+    if (t != ls_tile) {  // uniform
+      uint32_t oc0, g0, v0;
+      int x0;
+      tile_of(t, oc0, g0);
+      tpos(g0 < p.T ? g0 : 0u, v0, x0);
+#pragma unroll
+      for (int j = 0; j < SP; ++j) {  // piece: channel c, row s, column col of the [4][RIN][WPM] image
+        const uint32_t f = (uint32_t)((j * NW + wave) * 64 + lane) * PW;
+        const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
+        const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
+        const uint32_t v = v0 + s;
+        const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
+        const uint32_t iy = v - img * p.VH - p.py;  // wraps (misses) in the top padding
+        const bool ok = (c < (uint32_t)WCI) & (col < p.W) & (iy < p.H) & (img < p.B);
+        svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + col) * 4u);
+      }
+      ls_tile = t;
+    }
+    ss = ic0 * p.HW * 4u;
+    return it >= it1;
+  };
+  auto issue_strip = [&](int j, int sl, uint32_t ss, bool dead) {
+    float *const base = smem + sl * SLOT + GZ;
+    dma16s(dead ? rnull : rsi, base + (j * NW + wave) * 256, svo[j], ss);
+  };
+
+  // ---- U of stage it into registers: lane (li, lg) holds rows (channel ic0 + lg, output channel
+  // oc0 + wo*32 + 16a + li), chunk x from position co[x]
+  // one register buffer: group x of stage it+1 loads right after group x of stage it's MFMAs
+  f32x4v ur[2][4];
+  uint32_t uoff[2][4];
+  uint32_t lu_tile = 0xffffffffu;
+  auto plan_u = [&](uint32_t it) -> uint32_t {  // scalar offset of stage it's channels
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * WCI;
+    if (t != lu_tile) {  // uniform
+      uint32_t oc0, g0;
+      tile_of(t, oc0, g0);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + li);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) uoff[a][x] = oob_unless(oc < p.OC32, ((uint32_t)lg * p.OC32 + oc) * 64u + co[x] * 4u);
+      }
+      lu_tile = t;
+    }
+    return it < it1 ? ic0 * p.OC32 * 64u : 0x7fffff00u;  // dead stages: misses
+  };
+  auto load_u = [&](int x, uint32_t su) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+      ur[a][x] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[a][x], su, 0));
+  };
+
+  // ---- input transform: thread (cl, tt) of the first 4*TT, the patch of tile g0 + tt, channel cl
+  const uint32_t xcl = (uint32_t)tid / TT, xtt = (uint32_t)tid % TT;
+  uint32_t xb = GZ;
+  uint32_t xm = 0xfu;  // !V4: patch columns inside the row (the rest of a 16-B piece is the next row's)
+  uint32_t lx_tile = 0xffffffffu;
+  auto xplan = [&](uint32_t it) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    if (t == lx_tile) return;
+    lx_tile = t;
+    uint32_t oc0, g0, v0;
+    int x0;
+    tile_of(t, oc0, g0);
+    tpos(g0 < p.T ? g0 : 0u, v0, x0);
+    const uint32_t tg = g0 + xtt;
+    xb = GZ;
+    if (tg < p.T) {
+      uint32_t v;
+      int x;
+      tpos(tg, v, x);
+      xb = (uint32_t)((int)(GZ + xcl * p.RW + (v - v0) * p.WPM) + x);
+      xm = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xm |= ((uint32_t)(x + c) < p.W ? 1u : 0u) << c;
+    }
+  };
+  float d[4][4];
+  auto tx_read = [&](int sl) {
+    if (tid < WCI * TT) {
+      const float *const s = smem + sl * SLOT + xb;
+      const uint32_t wpm = p.WPM;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          d[r][c] = s[r * wpm + c];
+          if constexpr (!V4) d[r][c] = (xm >> c) & 1u ? d[r][c] : 0.0f;
+        }
+    }
+  };
+  auto tx_write = [&](int vb) {
+    if (tid < WCI * TT) {
+      float t[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t[0][c] = d[0][c] - d[2][c];
+        t[1][c] = d[1][c] + d[2][c];
+        t[2][c] = d[2][c] - d[1][c];
+        t[3][c] = d[1][c] - d[3][c];
+      }
+      float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
+      const uint32_t r2 = (xtt >> 2) & 3u;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const f32x4v v = {t[x][0] - t[x][2], t[x][1] + t[x][2], t[x][2] - t[x][1], t[x][1] - t[x][3]};
+        *(f32x4v *)(vd + ((x + r2) & 3u) * 4) = v;
+      }
+    }
+  };
+
+  // ---- V fragments (buffer vb), group x: column tile wtl*32 + 16b + li, channel lg; one register
+  // buffer like U
+  f32x4v vf[2][4];
+  auto vfrag = [&](int vb, int x) {
+    const float *const vp = vbase + vb * VSZ + (lg * TT + wtl * 32 + li) * 16;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) vf[b][x] = *(const f32x4v *)(vp + b * 256 + co[x]);
+  };
+
+  f32x4v acc[2][2][16];
+  auto mfma_x = [&](int x) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(ur[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
+  };
+
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+  auto out_q = [&](int q) -> f32x4v {
+    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
+    float s0[4], s1[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      float m0, m1, m2, m3;
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m0) : "a"(acc[a][b][n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m1) : "a"(acc[a][b][4 + n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m2) : "a"(acc[a][b][8 + n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m3) : "a"(acc[a][b][12 + n][j]));
+      s0[n] = m0 + m1 + m2;
+      s1[n] = m1 - m2 - m3;
+    }
+    return f32x4v{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]};
+  };
+  float bias[2][4];
+  uint32_t sob[2];
+  bool stv[2], sx1[2], sy1[2];
+  auto store_pos = [&](uint32_t g0) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
+      stv[b] = tg < p.T;
+      const uint32_t tgc = stv[b] ? tg : 0u;
+      const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
+      const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+      sx1[b] = 2 * tx + 1 < p.OW;
+      sy1[b] = 2 * ty + 1 < p.OH;
+      sob[b] = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
+    }
+  };
+  auto store_q = [&](uint32_t oc0, int q, f32x4v yy) {
+    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
+    const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
+    const bool ok = stv[b] & (oc < p.OC);
+    const uint32_t o = sob[b] + oc * p.OHW;
+    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1[b], (o + 1) * 4u),
+                             oob_unless(ok & sy1[b], (o + p.OW) * 4u),
+                             oob_unless(ok & sx1[b] & sy1[b], (o + p.OW + 1) * 4u)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float z = yy[e] + bias[a][j];
+      if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
+      z = (p.relu && z < 0.0f) ? 0.0f : z;
+      wg_store1(p, rso, (DBG & 8) ? OOB : off[e], z);
+    }
+  };
+  auto finish_tile = [&](uint32_t t) {
+    uint32_t oc0, g0;
+    tile_of(t, oc0, g0);
+    const uint32_t tb = t * p.ipt;
+    const bool whole = tb >= it0 && tb + p.ipt <= it1;  // uniform
+    store_pos(g0);
+    const uint32_t sl = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (NQ * NT * 4), NQ * NT * 16);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const f32x4v y = out_q(q);
+      if (whole)
+        store_q(oc0, q, y);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y), rw,
+                                               (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (whole) return;
+    const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t last = old == b1 - b0 ? 1u : 0u;
+      if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+    const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += 4) {
+      f32x4v y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      for (uint32_t b = b0; b <= b1; ++b) {  // block order = k order: bitwise reproducible
+        const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+        const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
+        f32x4v x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          x[i] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rall, base + (uint32_t)(((q0 + i) * NT + tid) * 16), 0, AUX_SC1));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] += x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) store_q(oc0, q0 + i, y[i]);
+    }
+  };
+
+#ifdef BH_KTRACE
+  uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t tk0 = __builtin_amdgcn_s_memtime();
+  uint64_t tkp = tk0;
+#endif
+
+  // ---- prologue: strips of stages it0 .. it0+D-1 and U(it0) in flight; V(it0), V(it0+1)
+  // transformed; stage it0+D's strip issued into stage it0's slot; V(it0)'s fragments read
+#pragma unroll
+  for (int s = 0; s < D; ++s) {
+    uint32_t ss;
+    const bool dead = plan_strip(it0 + (uint32_t)s, ss);
+#pragma unroll
+    for (int j = 0; j < SP; ++j) issue_strip(j, s, ss, dead);
+  }
+  {
+    const uint32_t su = plan_u(it0);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) load_u(x, su);
+  }
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  xplan(it0);
+  tx_read(0);
+  tx_write(0);
+  xplan(it0 + 1);
+  tx_read(1);
+  tx_write(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  {
+    uint32_t ss;
+    const bool dead = plan_strip(it0 + D, ss);
+#pragma unroll
+    for (int j = 0; j < SP; ++j) issue_strip(j, 0, ss, dead);
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x) vfrag(0, x);
+
+  // stage it: strips of it+2 .. it+D+1 in slots (it - it0 + 2 .. ) % D; V(it) in buffer it % 3
+  // (fragments in registers), V(it+1) complete, V(it+2) written this stage
+  int sl2 = 2 % D;  // slot of stage it+2
+  int vb = 0;       // V buffer of stage it (relative to it0)
+  // per stage and lane, VMEM in issue order: after MFMA group x, U(it+1) group x (2 loads) then
+  // strip share x of stage it+D+1 (QG DMAs); so U(it) group x has exactly 6 + SP younger loads when
+  // group x needs it, and stage it+2's strip (D-2) whole stages of 8 + SP at the top of stage it
+  auto stage = [&](uint32_t it) {
+    vm_wait<WTOP>();  // stage it+2's strip landed (this wave's DMAs)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's; V(it+1) written; V(it+2)'s buffer and stage it+1's slot free
+    asm volatile("" ::: "memory");
+#ifdef BH_KTRACE
+    { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); tk[1] += tn_ - tkp; tkp = tn_; tk[6] += 1; }
+#endif
+    const int vb1 = vb == 2 ? 0 : vb + 1, vb2 = vb1 == 2 ? 0 : vb1 + 1;
+    const int sl1 = sl2 == 0 ? D - 1 : sl2 - 1;  // slot of stage it+1 (its strip transformed last stage)
+    if constexpr ((DBG & 1) == 0) {
+      xplan(it + 2);
+      tx_read(sl2);
+    }
+    uint32_t ss = 0;
+    bool dead = true;
+    if constexpr ((DBG & 4) == 0) dead = plan_strip(it + D + 1, ss);
+    const uint32_t su = plan_u(it + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int QG = (SP + 3) / 4;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      vm_wait<6 + SP>();  // U(it) group x landed
+      if constexpr ((DBG & 2) == 0) mfma_x(x);
+      else acc[0][0][x] += ur[0][x] + vf[0][x];
+      __builtin_amdgcn_sched_barrier(0);
+      load_u(x, su);
+      vfrag(vb1, x);
+      if constexpr ((DBG & 4) == 0) {
+#pragma unroll
+        for (int j = x * QG; j < (x + 1) * QG; ++j) {
+          if (j < SP) issue_strip(j, sl1, ss, dead);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (x == 0) {
+        if constexpr ((DBG & 1) == 0) tx_write(vb2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#ifdef BH_KTRACE
+    { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); tk[4] += tn_ - tkp; tkp = tn_; }
+#endif
+    vb = vb1;
+    sl2 = sl2 == D - 1 ? 0 : sl2 + 1;
+  };
+
+  uint32_t it = it0;
+  while (it < it1) {
+    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+    const uint32_t iend = min(it1, (t + 1) * p.ipt);
+    {
+      uint32_t oc0, g0;
+      tile_of(t, oc0, g0);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
+          bias[a][j] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[a][b][q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    for (; it < iend; ++it) stage(it);
+#ifdef BH_KTRACE
+    tkp = __builtin_amdgcn_s_memtime();
+#endif
+    finish_tile(t);
+#ifdef BH_KTRACE
+    { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); tk[5] += tn_ - tkp; tkp = tn_; }
+#endif
+  }
+  vm_wait<0>();
+#ifdef BH_KTRACE
+  tk[7] = __builtin_amdgcn_s_memtime() - tk0;
+  if (tid == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p.trace[(size_t)blockIdx.x * 8 + i] = tk[i];
+  }
+#endif
+}
+
+template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
+cfg_t wgp_cfg(const char *name) {
+  cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgp_kernel<NWO, NWT, D, V4, SP, DBG>;
+  c.dc = 4;
+  c.dc_ky = 3;
+  c.dc_kx = 3;
+  c.dc_s = V4;
+  c.dc_rin = SP;
+  c.dc_ci = D;
+  c.dc_wpm = 1;  // pipelined form: LDS = strip slots + three V buffers (launch_wg)
+  return c;
+}
+
+template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
 cfg_t wg_cfg(const char *name) {
   cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wg_kernel<NWO, NWT, D, V4, SP>;
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wg_kernel<NWO, NWT, D, V4, SP, DBG>;
   c.dc = 4;
   c.dc_ky = 3;
   c.dc_kx = 3;
@@ -479,6 +1019,15 @@ std::vector<cfg_t> wg_cfgs() {
       wg_cfg<2, 2, 3, 1, 4>("wg64x64v"), wg_cfg<2, 2, 3, 0, 8>("wg64x64"),
       wg_cfg<2, 2, 4, 1, 3>("wg64x64vd4"), wg_cfg<2, 2, 4, 0, 6>("wg64x64d4"),
       wg_cfg<4, 1, 3, 1, 2>("wg128x32v"), wg_cfg<4, 1, 3, 0, 6>("wg128x32"),
+      // software-pipelined (U in registers, V triple-buffered)
+      wgp_cfg<2, 2, 3, 1, 4>("wgp64x64v"), wgp_cfg<2, 2, 3, 0, 3>("wgp64x64"),
+      wgp_cfg<2, 2, 4, 1, 3>("wgp64x64vd4"), wgp_cfg<2, 2, 4, 0, 3>("wgp64x64d4"),
+      wgp_cfg<4, 1, 3, 1, 2>("wgp128x32v"), wgp_cfg<4, 1, 3, 0, 2>("wgp128x32"),
+#ifdef BH_WG_DIAG
+      wg_cfg<2, 2, 3, 1, 4, 1>("xwg64x64v_noxf"), wg_cfg<2, 2, 3, 1, 4, 2>("xwg64x64v_nomfma"),
+      wg_cfg<2, 2, 3, 1, 4, 4>("xwg64x64v_nodma"), wg_cfg<2, 2, 3, 1, 4, 8>("xwg64x64v_nostore"),
+      wg_cfg<2, 2, 3, 1, 4, 7>("xwg64x64v_onlyskel"), wg_cfg<2, 2, 3, 1, 4, 3>("xwg64x64v_noxfmfma"),
+#endif
   };
 }
 
@@ -496,7 +1045,7 @@ int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uin
 
 // Launch a Winograd configuration: UNSUP unless a stride-1 3x3 conv with pad <= 1, IC % 4 == 0,
 // whose strips fit the configuration's slot. splits: 0 / 1..4 blocks per CU, iterations dealt
-// equally; 5..8: blocks per CU 1..4, whole tiles per block.
+// equally; 5..8: blocks per CU 1..4, whole tiles per block; + 10: OC tiles slowest.
 int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
               float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
               uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
@@ -520,7 +1069,8 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
     const uint32_t a = gi * TT, b = std::min(T, a + TT) - 1;
     rin = std::max(rin, vrow(b) + 4 - vrow(a));
   }
-  const uint32_t PW = c.dc_s ? 4 : 1, SP = (uint32_t)c.dc_rin;
+  const bool piped = c.dc_wpm != 0;  // wgp: strip-only slots, three V buffers, 16-B pieces always
+  const uint32_t PW = (c.dc_s || piped) ? 4 : 1, SP = (uint32_t)c.dc_rin;
   if ((uint64_t)WCI * rin * WPM > (uint64_t)SP * NT * PW)
     return bh::fail(BH_UNSUP, std::string("conv: input strip too large for ") + c.name);
   const uint64_t out_bytes = (uint64_t)B * out_ctot * OH * OW * 4;
@@ -548,14 +1098,19 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   p.relu = relu;
   p.wt = wt;
   // dynamic LDS: D slots (U + guard + strip), two V buffers, the ticket flag
-  const uint32_t slot = WCI * OCT * 16 + 4 + SP * NT * PW;
-  const uint32_t lds = (D * slot + 2 * WCI * TT * 16 + 4) * 4;
+  const uint32_t slot = (piped ? 0 : WCI * OCT * 16) + 4 + SP * NT * PW;
+  const uint32_t lds = (D * slot + (piped ? 3 : 2) * WCI * TT * 16 + 4) * 4;
   if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: LDS too small for ") + c.name);
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+  // splits: + 10 = OC tile slowest
+  p.ocs = splits >= 10 ? 1 : 0;
+  if (splits >= 10) splits -= 10;
+  p.ngr = ngroups;
+  f = bh::make_fastdiv(ngroups); p.ngr_m = f.m; p.ngr_s = f.s;
   const bool whole = splits > 4;
   uint32_t bpc = splits ? (whole ? splits - 4 : splits) : 1;
   bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
