@@ -18,22 +18,20 @@
 // MI355X structure (one fused kernel: nothing of U, V or M goes to HBM):
 //  * the filter transform is part of the filter-bank pack (bh_conv_filts_pack, Boda's
 //    xpose_filts role: once per net / op list, untimed as in the reference, src/rtc_prof.cc:93-99):
-//    U [IC4][OC32][16], each (ic, oc) row's four 4-float chunks rotated by (oc >> 2) & 3 so that
-//    16 lanes reading 16 consecutive output channels' chunk x with ds_read_b128 hit 16 distinct
-//    4-bank groups (conflict-free, MI355X_MICROARCH.md §LDS);
+//    U [IC4][OC32][16], each (ic, oc) row's four 4-float chunks rotated by (oc >> 2) & 3;
 //  * a block owns OCT = 32*NWO output channels x TT = 32*NWT Winograd tiles of the flattened
-//    (image, tile row, tile column) space; a stage is WCI = 4 input channels: the U slice
-//    [4][OCT][16] (16-B LDS-DMA) and the input strip [4][RIN][WPM] -- the "virtual" padded rows
-//    the tiles' patches touch (img*VH + iy + py, rows outside an image read as zero) at a pitch
-//    WPM > W whose zero tail also serves a patch's left neighbour (the previous row's tail);
-//  * per stage the block transforms the next stage's strip into V [4][TT][16] (one (channel,
-//    tile) pair per thread: 16 LDS reads, 32 adds, four ds_write_b128 at the same rotation), so
-//    each (tile, channel) is transformed once per block and shared by its NWO channel waves;
-//  * a wave owns 32 channels x 32 tiles x all 16 Winograd positions: v_mfma_f32_16x16x4_f32
-//    (exact fp32) with k = the stage's 4 channels, A = U (rows: channels), B = V (columns:
-//    tiles): 2 x 2 x 16 accumulator tiles (256 AGPRs, one wave per SIMD), 64 MFMAs per stage;
-//    every lane then holds all 16 positions of its (channel, tile) pairs, so the output
-//    transform, bias, residual and ReLU run in registers;
+//    (image, tile row, tile column) space; a stage is WCI = 4 input channels. The stage's input
+//    strip [4][RIN][WPM] -- the "virtual" padded rows the tiles' patches touch (img*VH + iy + py,
+//    rows outside an image read as zero) at a pitch WPM > W whose zero tail also serves a patch's
+//    left neighbour -- arrives by 16-B LDS-DMA in a D-slot ring;
+//  * stage it+2's patches are transformed during stage it into a triple-buffered V [4][TT][16]
+//    (each (tile, channel) once per block, shared by the NWO channel waves);
+//  * a wave owns 32 channels x 32 tiles x all 16 Winograd positions: v_mfma_f32_32x32x2_f32
+//    (exact fp32), A = U straight from L2 into registers, B = V fragments from LDS, both loaded
+//    for stage it+1 in four groups right after stage it's MFMA group that freed their registers;
+//    16 accumulator tiles (256 AGPRs, one wave per SIMD); every lane then holds all 16 positions
+//    of its (channel, tile) pairs, so the output transform, bias, residual and ReLU run in
+//    registers;
 //  * a persistent stream-K grid deals the (tile, stage) iterations equally between blocks (as
 //    bh_dcm.hip); a tile cut between blocks is summed after the output transform (linear) by
 //    its last-arriving block in block order: bitwise reproducible.
@@ -68,7 +66,7 @@ struct WgArgs {
 
 namespace {
 
-constexpr int WCI = 4;  // input channels per stage (the k of one 16x16x4 MFMA)
+constexpr int WCI = 4;  // input channels per stage (two k-steps of 32x32x2 MFMAs)
 
 // Filter transform: u[ic][oc][chunk rotated] = G g G^T for oc < OC32, ic < IC4 (zero past OC / IC)
 __global__ __launch_bounds__(256) void wino_pack_kernel(const float *__restrict__ w, float *__restrict__ u,
@@ -111,440 +109,9 @@ __device__ __forceinline__ void wg_store1(const WgArgs &p, __amdgpu_buffer_rsrc_
   else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_OUT);
 }
 
-// NWO x NWT waves (32 channels x 32 tiles each); D-slot DMA ring (D >= 3); V4: 16-B strip pieces
-// (W % 4 == 0); SP: strip DMA pieces per thread and stage (the slot's strip capacity)
-// DBG (diagnostic builds only; wrong results by design): bit 0 = no input transform in the loop,
-// bit 1 = no MFMA, bit 2 = no DMA after the prologue, bit 3 = no output stores
-template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
-__global__ __launch_bounds__(64 * NWO * NWT) void wg_kernel(WgArgs p) {
-  constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT;
-  constexpr int UF = WCI * OCT * 16;          // U floats per slot
-  static_assert(UF % (4 * NT) == 0, "whole U pieces per thread");
-  constexpr int LWU = UF / (4 * NT);          // 16-B U pieces per thread and stage
-  constexpr int PW = V4 ? 4 : 1;              // floats per strip piece
-  constexpr int SCAP = SP * NT * PW;          // strip floats per slot
-  constexpr int GZ = 4;                       // zero guard before the strip (a patch's left neighbour of row 0)
-  constexpr int SLOT = UF + GZ + SCAP;
-  constexpr int VSZ = WCI * TT * 16;          // floats of one V buffer
-  constexpr int LW = LWU + SP;
-  constexpr int NQ = 16;                      // float4 results per lane: (a, b, j)
-  static_assert(D >= 3 && (D - 3) * LW <= 63, "vmcnt range");
-  static_assert(WCI * TT <= NT, "one transform pair per thread");
-  static_assert((SLOT % 4) == 0 && (UF + GZ) % 4 == 0, "16-B aligned slot parts");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float *const vbase = smem + D * SLOT;
-  uint32_t *const flag = (uint32_t *)(vbase + 2 * VSZ);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wo = wave % NWO, wtl = wave / NWO;
-  const int li = lane & 15, lg = lane >> 4;
-  const uint32_t lb = wg_lb(blockIdx.x, gridDim.x);
-  const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
-  if (tid < D * GZ) smem[(tid / GZ) * SLOT + UF + tid % GZ] = 0.0f;
-
-  // tile t = (tile group, OC tile), OC tile fastest (consecutive tiles share the strip via L2)
-  // tile t = (tile group, OC tile): OC tile fastest (consecutive tiles share the strip through L2),
-  // or slowest (ocs: an XCD's run of tiles shares one OC tile's U slice -- U outgrows the L2 where
-  // IC*OC is large)
-  auto tile_of = [&](uint32_t t, uint32_t &oc0, uint32_t &g0) {
-    if (p.ocs) {
-      const uint32_t q = fdiv(t, p.ngr_m, p.ngr_s);
-      oc0 = q * OCT;
-      g0 = (t - q * p.ngr) * TT;
-    } else {
-      const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
-      oc0 = (t - pt * p.tiles_m) * OCT;
-      g0 = pt * TT;
-    }
-  };
-  // Winograd tile tg: virtual strip row of its patch's top, its patch's first input column
-  auto tpos = [&](uint32_t tg, uint32_t &v, int &x) {
-    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
-    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
-    v = img * p.VH + 2 * ty;
-    x = 2 * (int)tx - (int)p.px;
-  };
-
-  // ---- DMA sources: tile-independent per-lane parts
-  const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
-  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
-  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
-  uint32_t urel[LWU];
-#pragma unroll
-  for (int j = 0; j < LWU; ++j) {  // piece e of the [4][OCT][16] slice: channel c, floats 4r .. of its OCT*16 run
-    const uint32_t e = (uint32_t)((j * NW + wave) * 64 + lane), c = e / (4 * OCT), r = e % (4 * OCT);
-    urel[j] = (c * p.OC32 * 16 + r * 4) * 4;
-  }
-  uint32_t uvo[LWU], svo[SP];
-  uint32_t ls_tile = 0xffffffffu;
-  // scalar parts of iteration it (tile it / ipt, channel group it % ipt); true: a dead stage
-  auto plan = [&](uint32_t it, uint32_t &su, uint32_t &ss) -> bool {
-    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s), ic0 = (it - t * p.ipt) * WCI;
-    if (t != ls_tile) {  // uniform
-      uint32_t oc0, g0;
-      tile_of(t, oc0, g0);
-#pragma unroll
-      for (int j = 0; j < LWU; ++j) uvo[j] = urel[j] + oc0 * 64u;
-      uint32_t v0;
-      int x0;
-      tpos(g0 < p.T ? g0 : 0u, v0, x0);
-#pragma unroll
-      for (int j = 0; j < SP; ++j) {  // strip piece: channel c, row s, column col of the [4][RIN][WPM] image
-        const uint32_t f = (uint32_t)((j * NW + wave) * 64 + lane) * PW;
-        const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
-        const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
-        const uint32_t v = v0 + s;
-        const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
-        const uint32_t iy = v - img * p.VH - p.py;  // wraps (misses) in the top padding
-        const bool ok = (c < (uint32_t)WCI) & (col < p.W) & (iy < p.H) & (img < p.B);
-        svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + col) * 4u);
-      }
-      ls_tile = t;
-    }
-    su = ic0 * p.OC32 * 64u;
-    ss = ic0 * p.HW * 4u;
-    return it >= it1;
-  };
-  auto issue_one = [&](int q, int slot, uint32_t su, uint32_t ss, bool dead) {
-    float *const base = smem + slot * SLOT;
-    if (q < LWU) {
-      dma16s(dead ? rnull : rsu, base + (q * NW + wave) * 256, uvo[q], su);
-    } else {
-      const int j = q - LWU;
-      if constexpr (V4) dma16s(dead ? rnull : rsi, base + UF + GZ + (j * NW + wave) * 256, svo[j], ss);
-      else dma4s(dead ? rnull : rsi, base + UF + GZ + (j * NW + wave) * 64, svo[j], ss);
-    }
-  };
-
-  // ---- input transform: thread (cl, tt) of the first 4*TT, the patch of tile g0 + tt, channel cl
-  const uint32_t xcl = (uint32_t)tid / TT, xtt = (uint32_t)tid % TT;
-  uint32_t xb = GZ;  // the patch's first float in the strip (guard included)
-  uint32_t lx_tile = 0xffffffffu;
-  auto xplan = [&](uint32_t it) {
-    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
-    if (t == lx_tile) return;
-    lx_tile = t;
-    uint32_t oc0, g0;
-    tile_of(t, oc0, g0);
-    uint32_t v0;
-    int x0;
-    tpos(g0 < p.T ? g0 : 0u, v0, x0);
-    const uint32_t tg = g0 + xtt;
-    xb = GZ;
-    if (tg < p.T) {
-      uint32_t v;
-      int x;
-      tpos(tg, v, x);
-      xb = (uint32_t)((int)(GZ + xcl * p.RW + (v - v0) * p.WPM) + x);
-    }
-  };
-  // split in two so the reads go out with the stage's fragment reads and the adds sit between MFMA
-  // groups: the 4x4 patch into d, then B^T d B into V
-  float d[4][4];
-  auto tx_read = [&](int sl) {
-    if (tid < WCI * TT) {
-      const float *const s = smem + sl * SLOT + UF + xb;
-      const uint32_t wpm = p.WPM;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) d[r][c] = s[r * wpm + c];
-    }
-  };
-  auto tx_write = [&](int vb) {
-    if (tid < WCI * TT) {
-      float t[4][4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        t[0][c] = d[0][c] - d[2][c];
-        t[1][c] = d[1][c] + d[2][c];
-        t[2][c] = d[2][c] - d[1][c];
-        t[3][c] = d[1][c] - d[3][c];
-      }
-      float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
-      const uint32_t rot = (xtt >> 2) & 3u;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const f32x4v v = {t[x][0] - t[x][2], t[x][1] + t[x][2], t[x][2] - t[x][1], t[x][1] - t[x][3]};
-        *(f32x4v *)(vd + ((x + rot) & 3u) * 4) = v;
-      }
-    }
-  };
-  auto transform = [&](int sl, int vb) {
-    tx_read(sl);
-    tx_write(vb);
-  };
-
-  // ---- MFMA stage: lane (li, lg): channel k = lg of the stage; A row = output channel
-  // oc0 + wo*32 + 16a + li, B column = tile wtl*32 + 16b + li; chunk x of its 16 positions sits at
-  // ((x + rot) & 3) * 4 (the same rotation for U and V: (li >> 2) & 3)
-  f32x4v acc[2][2][16];
-  const uint32_t rot = ((uint32_t)li >> 2) & 3u;
-  uint32_t co[4];
-#pragma unroll
-  for (int x = 0; x < 4; ++x) co[x] = ((x + rot) & 3u) * 4u;
-  // the stage's 16 fragment reads go out together (one LDS round trip), then the MFMAs in x order
-  // (x's group waits only for its own reads); hipcc otherwise issues each read just before its
-  // MFMAs and waits on every one
-  f32x4v uf[2][4], vf[2][4];
-  auto frags = [&](int sl, int vb) {
-    const float *const ub = smem + sl * SLOT + (lg * OCT + wo * 32 + li) * 16;
-    const float *const vp = vbase + vb * VSZ + (lg * TT + wtl * 32 + li) * 16;
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        uf[a][x] = *(const f32x4v *)(ub + a * 256 + co[x]);
-        vf[a][x] = *(const f32x4v *)(vp + a * 256 + co[x]);
-      }
-  };
-  auto mfma_x = [&](int x) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
-  };
-
-  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
-  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
-  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
-
-  // output transform of accumulator group q = (a*2 + b)*4 + j: {y00, y01, y10, y11} of output
-  // channel oc0 + wo*32 + 16a + 4lg + j, tile wtl*32 + 16b + li
-  auto out_q = [&](int q) -> f32x4v {
-    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
-    float s0[4], s1[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      // explicit AGPR reads at this point: hipcc otherwise copies all 256 accumulators to VGPRs at
-      // the loop exit, and the epilogue spills
-      float m0, m1, m2, m3;
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m0) : "a"(acc[a][b][n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m1) : "a"(acc[a][b][4 + n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m2) : "a"(acc[a][b][8 + n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m3) : "a"(acc[a][b][12 + n][j]));
-      s0[n] = m0 + m1 + m2;
-      s1[n] = m1 - m2 - m3;
-    }
-    return f32x4v{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]};
-  };
-  // bias (prefetched per tile), residual, ReLU and masked stores of group q's results
-  float bias[2][4];
-  // a tile's output positions, once per tile (b: column tile): image base + (2ty, 2tx) offset,
-  // and which of the 2x2 outputs exist (odd OH / OW, tiles past the op)
-  uint32_t sob[2];
-  bool stv[2], sx1[2], sy1[2];
-  auto store_pos = [&](uint32_t g0) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
-      stv[b] = tg < p.T;
-      const uint32_t tgc = stv[b] ? tg : 0u;
-      const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
-      const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
-      sx1[b] = 2 * tx + 1 < p.OW;
-      sy1[b] = 2 * ty + 1 < p.OH;
-      sob[b] = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
-    }
-  };
-  auto store_q = [&](uint32_t oc0, int q, f32x4v yy) {
-    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
-    const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
-    const bool ok = stv[b] & (oc < p.OC);
-    const uint32_t o = sob[b] + oc * p.OHW;
-    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1[b], (o + 1) * 4u),
-                             oob_unless(ok & sy1[b], (o + p.OW) * 4u),
-                             oob_unless(ok & sx1[b] & sy1[b], (o + p.OW + 1) * 4u)};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float z = yy[e] + bias[a][j];
-      if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
-      z = (p.relu && z < 0.0f) ? 0.0f : z;
-      wg_store1(p, rso, (DBG & 8) ? OOB : off[e], z);
-    }
-  };
-  // tile t done in this block: store it, or hand the partial tile over through this block's slab
-  // and the tile's ticket (the last arriver sums the slabs in block order)
-  auto finish_tile = [&](uint32_t t) {
-    uint32_t oc0, g0;
-    tile_of(t, oc0, g0);
-    const uint32_t tb = t * p.ipt;
-    const bool whole = tb >= it0 && tb + p.ipt <= it1;  // uniform
-    store_pos(g0);
-    const uint32_t sl = (t == fdiv(it0, p.ipt_m, p.ipt_s)) ? 0u : 1u;
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (NQ * NT * 4), NQ * NT * 16);
-    // one group at a time: its 16 accumulators out of the AGPRs, transformed, stored (whole tile)
-    // or written to the slab (hipcc otherwise reads all 256 AGPRs before the branch and spills)
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const f32x4v y = out_q(q);
-      if (whole)
-        store_q(oc0, q, y);
-      else
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, y), rw,
-                                               (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (whole) return;
-    const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t last = old == b1 - b0 ? 1u : 0u;
-      if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
-    const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
-    // four result groups at a time, every block's slab of them in flight, summed in block order
-    // (block order = k order: bitwise reproducible)
-#pragma unroll
-    for (int q0 = 0; q0 < NQ; q0 += 4) {
-      f32x4v y[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-      for (uint32_t b = b0; b <= b1; ++b) {
-        const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
-        const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
-        f32x4v x[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          x[i] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rall, base + (uint32_t)(((q0 + i) * NT + tid) * 16), 0, AUX_SC1));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] += x[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) store_q(oc0, q0 + i, y[i]);
-    }
-  };
-
-#ifdef BH_KTRACE
-  // per-phase shader-clock sums (s_memtime; its lgkmcnt wait distorts LDS overlap a little):
-  // [0] 0, [1] wait + barrier, [2] DMA issue, [3] fragment reads + input transform, [4] MFMA issue,
-  // [5] tile epilogues, [6] iterations, [7] whole block
-  uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t tk0 = __builtin_amdgcn_s_memtime();
-  uint64_t tkp = tk0;
-#define TK(i)                                                   \
-  do {                                                          \
-    const uint64_t tn_ = __builtin_amdgcn_s_memtime();          \
-    tk[i] += tn_ - tkp;                                         \
-    tkp = tn_;                                                  \
-  } while (0)
-#else
-#define TK(i) \
-  do {        \
-  } while (0)
-#endif
-  // ---- prologue: stages it0 .. it0+D-2 in flight; the first stage's strip transformed
-#pragma unroll
-  for (int s = 0; s < D - 1; ++s) {
-    uint32_t su, ss;
-    const bool dead = plan(it0 + (uint32_t)s, su, ss);
-#pragma unroll
-    for (int q = 0; q < LW; ++q) issue_one(q, s, su, ss, dead);
-  }
-  vm_wait<(D - 2) * LW>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // stage it0 landed for every wave (and the guards are written)
-  asm volatile("" ::: "memory");
-  xplan(it0);
-  transform(0, 0);
-  int slot = 0, vb = 0;
-  uint32_t it = it0;
-  while (it < it1) {
-    const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
-    const uint32_t iend = min(it1, (t + 1) * p.ipt);
-    {
-      uint32_t oc0, g0;
-      tile_of(t, oc0, g0);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
-          bias[a][j] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[a][b][q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-    for (; it < iend; ++it) {
-#ifdef BH_KTRACE
-      tkp = __builtin_amdgcn_s_memtime();
-      tk[6] += 1;
-#endif
-      vm_wait<(D - 3) * LW>();  // stage it+1 landed (this wave's DMAs)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // ... every wave's; V(it) written; slot of it-1 and V(it+1)'s buffer free
-      asm volatile("" ::: "memory");
-      TK(1);
-      // the next stage's patch reads, this stage's fragment reads, then four MFMA groups with the
-      // stage it+D-1 DMAs and the patch's transform between them (their issue and latency under
-      // the MFMAs)
-      const int nslot = slot == D - 1 ? 0 : slot + 1, islot = slot == 0 ? D - 1 : slot - 1;
-      if constexpr ((DBG & 1) == 0) {
-        xplan(it + 1);
-        tx_read(nslot);
-      }
-      frags(slot, vb);
-      uint32_t su = 0, ss = 0;
-      bool dead = true;
-      if constexpr ((DBG & 4) == 0) dead = plan(it + D - 1, su, ss);
-      __builtin_amdgcn_sched_barrier(0);
-      TK(2);
-      constexpr int QG = (LW + 3) / 4;  // DMA issues per MFMA group
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        if constexpr ((DBG & 2) == 0) mfma_x(x);
-        else acc[0][0][x] += uf[0][x] + vf[0][x] + uf[1][x] + vf[1][x];
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr ((DBG & 4) == 0) {
-#pragma unroll
-          for (int q = x * QG; q < (x + 1) * QG && q < LW; ++q) issue_one(q, islot, su, ss, dead);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (x == 0) {
-          if constexpr ((DBG & 1) == 0) tx_write(vb ^ 1);
-          __builtin_amdgcn_sched_barrier(0);
-          TK(3);
-        }
-      }
-      TK(4);
-      slot = slot == D - 1 ? 0 : slot + 1;
-      vb ^= 1;
-    }
-#ifdef BH_KTRACE
-    tkp = __builtin_amdgcn_s_memtime();
-#endif
-    finish_tile(t);
-    TK(5);
-  }
-  vm_wait<0>();
-#ifdef BH_KTRACE
-  tk[7] = __builtin_amdgcn_s_memtime() - tk0;
-  if (tid == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) p.trace[(size_t)blockIdx.x * 8 + i] = tk[i];
-  }
-#endif
-}
-
-// wgp_kernel: the same Winograd stage, software-pipelined so that nothing but the barrier sits
-// between one stage's MFMAs and the next (the phase timings of wg_kernel, tools/wg_phases.py: per
-// stage ~2000 MFMA cycles beside ~1000 of LDS-read latency after the barrier and ~700 of LDS-DMA
-// issue):
+// wgp_kernel: a Winograd stage software-pipelined so that nothing but the barrier sits between one
+// stage's MFMAs and the next (a first, unpipelined form spent per stage ~2000 MFMA cycles beside
+// ~1000 of LDS-read latency after the barrier and ~700 of LDS-DMA issue, tools/wg_phases.py):
 //  * U goes straight from L2 into registers (16-B loads of the lane's own [4 channels][16] rows;
 //    group x of stage it+1 right after group x of stage it's MFMAs) -- no LDS slot, no DMA, no
 //    ds_read for it;
@@ -564,7 +131,10 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   constexpr int NQ = 16;                      // float4 results per lane: (a, b, j)
   constexpr int WTOP = (D - 2) * (SP + NU);  // younger than stage it+2's strip at the top
   static_assert(D >= 3 && WTOP <= 63, "vmcnt range");
-  static_assert(WCI * TT <= NT, "one transform pair per thread");
+  // the stage's WCI*TT patch transforms are spread over all NT threads: TS threads per patch, each
+  // producing 4 / TS rows xi of V (every wave takes the same share of the VALU work)
+  constexpr int TS = NT / (WCI * TT);
+  static_assert(TS == 1 || TS == 2, "one or two threads per patch");
   static_assert(SLOT % 4 == 0, "16-B aligned slots");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *const vbase = smem + D * SLOT;
@@ -573,7 +143,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wo = wave % NWO, wtl = wave / NWO;
-  const int li = lane & 15, lg = lane >> 4;
+  const int li = lane & 31, kh = lane >> 5;
   const uint32_t lb = wg_lb(blockIdx.x, gridDim.x);
   const uint32_t it0 = lb * p.ipb, it1 = min(p.total_it, it0 + p.ipb);
   if (tid < D * GZ) smem[(tid / GZ) * SLOT + tid % GZ] = 0.0f;
@@ -602,7 +172,10 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
   const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
   const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
-  // lane (li, lg): chunk x of its 16 positions sits at ((x + rot) & 3) * 4 in U's and V's rows
+  // v_mfma_f32_32x32x2_f32, lane (li, kh): A row = output channel oc0 + wo*32 + li, B column = tile
+  // wtl*32 + li, k = channel ic0 + 2s + kh at k step s of the stage; chunk x of a row's 16
+  // positions sits at ((x + rot) & 3) * 4 in U's and V's rows (a 16x16x4 form of this kernel ran
+  // its 64 MFMAs per stage at ~51 cycles each instead of 32: tools/wg_phases.py, xwgp_onlymfma)
   const uint32_t rot = ((uint32_t)li >> 2) & 3u;
   uint32_t co[4];
 #pragma unroll
@@ -639,9 +212,9 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     dma16s(dead ? rnull : rsi, base + (j * NW + wave) * 256, svo[j], ss);
   };
 
-  // ---- U of stage it into registers: lane (li, lg) holds rows (channel ic0 + lg, output channel
-  // oc0 + wo*32 + 16a + li), chunk x from position co[x]
-  // one register buffer: group x of stage it+1 loads right after group x of stage it's MFMAs
+  // ---- U of stage it into registers: lane (li, kh) holds rows (channel ic0 + 2s + kh, output
+  // channel oc0 + wo*32 + li), chunk x from position co[x]; one register buffer: group g of stage
+  // it+1 (k step s = g >> 1, chunks 2 (g & 1) .. + 1) loads right after group g of stage it's MFMAs
   f32x4v ur[2][4];
   uint32_t uoff[2][4];
   uint32_t lu_tile = 0xffffffffu;
@@ -650,24 +223,27 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     if (t != lu_tile) {  // uniform
       uint32_t oc0, g0;
       tile_of(t, oc0, g0);
+      const uint32_t oc = oc0 + (uint32_t)(wo * 32 + li);
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + li);
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int x = 0; x < 4; ++x) uoff[a][x] = oob_unless(oc < p.OC32, ((uint32_t)lg * p.OC32 + oc) * 64u + co[x] * 4u);
-      }
+        for (int x = 0; x < 4; ++x)
+          uoff[st][x] = oob_unless(oc < p.OC32, ((uint32_t)(2 * st + kh) * p.OC32 + oc) * 64u + co[x] * 4u);
       lu_tile = t;
     }
     return it < it1 ? ic0 * p.OC32 * 64u : 0x7fffff00u;  // dead stages: misses
   };
-  auto load_u = [&](int x, uint32_t su) {
+  auto load_u = [&](int g, uint32_t su) {
+    const int st = g >> 1;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-      ur[a][x] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[a][x], su, 0));
+    for (int x = 2 * (g & 1); x < 2 * (g & 1) + 2; ++x)
+      ur[st][x] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[st][x], su, 0));
   };
 
   // ---- input transform: thread (cl, tt) of the first 4*TT, the patch of tile g0 + tt, channel cl
-  const uint32_t xcl = (uint32_t)tid / TT, xtt = (uint32_t)tid % TT;
+  // (half h = tid / (4 TT): wave-uniform, so the two halves' different arithmetic does not diverge)
+  const uint32_t xpr = (uint32_t)tid % (WCI * TT), xh = __builtin_amdgcn_readfirstlane((uint32_t)tid / (WCI * TT));
+  const uint32_t xcl = xpr / TT, xtt = xpr % TT;
   uint32_t xb = GZ;
   uint32_t xm = 0xfu;  // !V4: patch columns inside the row (the rest of a 16-B piece is the next row's)
   uint32_t lx_tile = 0xffffffffu;
@@ -691,22 +267,33 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
       for (int c = 0; c < 4; ++c) xm |= ((uint32_t)(x + c) < p.W ? 1u : 0u) << c;
     }
   };
-  float d[4][4];
+  // TS == 1: patch rows 0..3, all four V rows; TS == 2: half h reads rows h .. h + 2 (d[0..2]) and
+  // makes V rows 2h, 2h + 1 (B^T rows 0, 1 use d0 - d2, d1 + d2; rows 2, 3 use d2 - d1, d1 - d3)
+  constexpr int NR = TS == 1 ? 4 : 3;
+  float d[NR][4];
   auto tx_read = [&](int sl) {
-    if (tid < WCI * TT) {
-      const float *const s = smem + sl * SLOT + xb;
-      const uint32_t wpm = p.WPM;
+    const float *const s = smem + sl * SLOT + xb + (TS == 2 ? xh * p.WPM : 0u);
+    const uint32_t wpm = p.WPM;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          d[r][c] = s[r * wpm + c];
-          if constexpr (!V4) d[r][c] = (xm >> c) & 1u ? d[r][c] : 0.0f;
-        }
-    }
+      for (int c = 0; c < 4; ++c) d[r][c] = s[r * wpm + c];
   };
   auto tx_write = [&](int vb) {
-    if (tid < WCI * TT) {
+    // (the masks here, not in tx_read: hipcc would wait for the reads before the first MFMA group)
+    if constexpr (!V4) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[r][c] = (xm >> c) & 1u ? d[r][c] : 0.0f;
+    }
+    float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
+    const uint32_t r2 = (xtt >> 2) & 3u;
+    auto put = [&](uint32_t x, const float (&t)[4]) {
+      const f32x4v v = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+      *(f32x4v *)(vd + ((x + r2) & 3u) * 4) = v;
+    };
+    if constexpr (TS == 1) {
       float t[4][4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -715,81 +302,92 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
         t[2][c] = d[2][c] - d[1][c];
         t[3][c] = d[1][c] - d[3][c];
       }
-      float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
-      const uint32_t r2 = (xtt >> 2) & 3u;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const f32x4v v = {t[x][0] - t[x][2], t[x][1] + t[x][2], t[x][2] - t[x][1], t[x][1] - t[x][3]};
-        *(f32x4v *)(vd + ((x + r2) & 3u) * 4) = v;
+      for (int x = 0; x < 4; ++x) put((uint32_t)x, t[x]);
+    } else {
+      // h = 0: rows 0..2 in d -> t0 = d0 - d2, t1 = d1 + d2; h = 1: rows 1..3 -> t2 = d1 - d0, t3 = d0 - d2
+      float ta[4], tb[4];
+      if (xh) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          ta[c] = d[1][c] - d[0][c];
+          tb[c] = d[0][c] - d[2][c];
+        }
+        put(2, ta);
+        put(3, tb);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          ta[c] = d[0][c] - d[2][c];
+          tb[c] = d[1][c] + d[2][c];
+        }
+        put(0, ta);
+        put(1, tb);
       }
     }
   };
 
-  // ---- V fragments (buffer vb), group x: column tile wtl*32 + 16b + li, channel lg; one register
-  // buffer like U
+  // ---- V fragments (buffer vb), group g: tile wtl*32 + li, channel 2s + kh; one register buffer
+  // like U
   f32x4v vf[2][4];
-  auto vfrag = [&](int vb, int x) {
-    const float *const vp = vbase + vb * VSZ + (lg * TT + wtl * 32 + li) * 16;
+  auto vfrag = [&](int vb, int g) {
+    const int st = g >> 1;
+    const float *const vp = vbase + vb * VSZ + ((2 * st + kh) * TT + wtl * 32 + li) * 16;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) vf[b][x] = *(const f32x4v *)(vp + b * 256 + co[x]);
+    for (int x = 2 * (g & 1); x < 2 * (g & 1) + 2; ++x) vf[st][x] = *(const f32x4v *)(vp + co[x]);
   };
 
-  f32x4v acc[2][2][16];
-  auto mfma_x = [&](int x) {
+  f32x16 acc[16];  // position p = 4 xi + nu
+  auto mfma_x = [&](int g) {
+    const int st = g >> 1;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int x = 2 * (g & 1); x < 2 * (g & 1) + 2; ++x)
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          acc[a][b][4 * x + n] = __builtin_amdgcn_mfma_f32_16x16x4f32(ur[a][x][n], vf[b][x][n], acc[a][b][4 * x + n], 0, 0, 0);
+      for (int n = 0; n < 4; ++n)
+        acc[4 * x + n] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[st][x][n], vf[st][x][n], acc[4 * x + n], 0, 0, 0);
   };
 
   const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+  // output transform of accumulator element q (output channel oc0 + wo*32 + 8 (q >> 2) + 4 kh + (q & 3),
+  // tile wtl*32 + li): {y00, y01, y10, y11}
   auto out_q = [&](int q) -> f32x4v {
-    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
     float s0[4], s1[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       float m0, m1, m2, m3;
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m0) : "a"(acc[a][b][n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m1) : "a"(acc[a][b][4 + n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m2) : "a"(acc[a][b][8 + n][j]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m3) : "a"(acc[a][b][12 + n][j]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m0) : "a"(acc[n][q]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m1) : "a"(acc[4 + n][q]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m2) : "a"(acc[8 + n][q]));
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(m3) : "a"(acc[12 + n][q]));
       s0[n] = m0 + m1 + m2;
       s1[n] = m1 - m2 - m3;
     }
     return f32x4v{s0[0] + s0[1] + s0[2], s0[1] - s0[2] - s0[3], s1[0] + s1[1] + s1[2], s1[1] - s1[2] - s1[3]};
   };
-  float bias[2][4];
-  uint32_t sob[2];
-  bool stv[2], sx1[2], sy1[2];
+  float bias[16];
+  uint32_t sob;
+  bool stv, sx1, sy1;
   auto store_pos = [&](uint32_t g0) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const uint32_t tg = g0 + (uint32_t)(wtl * 32 + 16 * b + li);
-      stv[b] = tg < p.T;
-      const uint32_t tgc = stv[b] ? tg : 0u;
-      const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
-      const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
-      sx1[b] = 2 * tx + 1 < p.OW;
-      sy1[b] = 2 * ty + 1 < p.OH;
-      sob[b] = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
-    }
+    const uint32_t tg = g0 + (uint32_t)(wtl * 32 + li);
+    stv = tg < p.T;
+    const uint32_t tgc = stv ? tg : 0u;
+    const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    sx1 = 2 * tx + 1 < p.OW;
+    sy1 = 2 * ty + 1 < p.OH;
+    sob = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
   };
   auto store_q = [&](uint32_t oc0, int q, f32x4v yy) {
-    const int a = q >> 3, b = (q >> 2) & 1, j = q & 3;
-    const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
-    const bool ok = stv[b] & (oc < p.OC);
-    const uint32_t o = sob[b] + oc * p.OHW;
-    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1[b], (o + 1) * 4u),
-                             oob_unless(ok & sy1[b], (o + p.OW) * 4u),
-                             oob_unless(ok & sx1[b] & sy1[b], (o + p.OW + 1) * 4u)};
+    const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 8 * (q >> 2) + 4 * kh + (q & 3));
+    const bool ok = stv & (oc < p.OC);
+    const uint32_t o = sob + oc * p.OHW;
+    const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1, (o + 1) * 4u),
+                             oob_unless(ok & sy1, (o + p.OW) * 4u), oob_unless(ok & sx1 & sy1, (o + p.OW + 1) * 4u)};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float z = yy[e] + bias[a][j];
+      float z = yy[e] + bias[q];
       if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
       z = (p.relu && z < 0.0f) ? 0.0f : z;
       wg_store1(p, rso, (DBG & 8) ? OOB : off[e], z);
@@ -900,7 +498,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   auto stage = [&](uint32_t it) {
     vm_wait<WTOP>();  // stage it+2's strip landed (this wave's DMAs)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's; V(it+1) written; V(it+2)'s buffer and stage it+1's slot free
+    if constexpr ((DBG & 128) == 0) __builtin_amdgcn_s_barrier();  // every wave's; V(it+1) written; V(it+2)'s buffer and stage it+1's slot free
     asm volatile("" ::: "memory");
 #ifdef BH_KTRACE
     { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); tk[1] += tn_ - tkp; tkp = tn_; tk[6] += 1; }
@@ -919,12 +517,12 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     constexpr int QG = (SP + 3) / 4;
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      vm_wait<6 + SP>();  // U(it) group x landed
+      if constexpr ((DBG & 64) == 0) vm_wait<6 + SP>();  // U(it) group x landed
       if constexpr ((DBG & 2) == 0) mfma_x(x);
-      else acc[0][0][x] += ur[0][x] + vf[0][x];
+      else acc[x][0] += ur[0][x][0] + vf[0][x][0];
       __builtin_amdgcn_sched_barrier(0);
-      load_u(x, su);
-      vfrag(vb1, x);
+      if constexpr ((DBG & 16) == 0) load_u(x, su);
+      if constexpr ((DBG & 32) == 0) vfrag(vb1, x);
       if constexpr ((DBG & 4) == 0) {
 #pragma unroll
         for (int j = x * QG; j < (x + 1) * QG; ++j) {
@@ -952,19 +550,15 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
       uint32_t oc0, g0;
       tile_of(t, oc0, g0);
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 16 * a + 4 * lg + j);
-          bias[a][j] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
-        }
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 8 * (q >> 2) + 4 * kh + (q & 3));
+        bias[q] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+      }
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int q = 0; q < 16; ++q)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[a][b][q] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
     for (; it < iend; ++it) stage(it);
 #ifdef BH_KTRACE
     tkp = __builtin_amdgcn_s_memtime();
@@ -994,39 +588,25 @@ cfg_t wgp_cfg(const char *name) {
   c.dc_s = V4;
   c.dc_rin = SP;
   c.dc_ci = D;
-  c.dc_wpm = 1;  // pipelined form: LDS = strip slots + three V buffers (launch_wg)
-  return c;
-}
-
-template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
-cfg_t wg_cfg(const char *name) {
-  cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wg_kernel<NWO, NWT, D, V4, SP, DBG>;
-  c.dc = 4;
-  c.dc_ky = 3;
-  c.dc_kx = 3;
-  c.dc_s = V4;
-  c.dc_rin = SP;
-  c.dc_ci = D;
   return c;
 }
 
 }  // namespace
 
 std::vector<cfg_t> wg_cfgs() {
-  // <NWO, NWT, D, V4, SP>: OCT = 32 NWO channels x TT = 32 NWT tiles; SP strip pieces per thread
+  // <NWO, NWT, D, V4, SP>: OCT = 32 NWO channels x TT = 32 NWT tiles; D strip slots; V4: W % 4 == 0
+  // (no row masks); SP strip DMA pieces per thread and stage
   return {
-      wg_cfg<2, 2, 3, 1, 4>("wg64x64v"), wg_cfg<2, 2, 3, 0, 8>("wg64x64"),
-      wg_cfg<2, 2, 4, 1, 3>("wg64x64vd4"), wg_cfg<2, 2, 4, 0, 6>("wg64x64d4"),
-      wg_cfg<4, 1, 3, 1, 2>("wg128x32v"), wg_cfg<4, 1, 3, 0, 6>("wg128x32"),
-      // software-pipelined (U in registers, V triple-buffered)
       wgp_cfg<2, 2, 3, 1, 4>("wgp64x64v"), wgp_cfg<2, 2, 3, 0, 3>("wgp64x64"),
       wgp_cfg<2, 2, 4, 1, 3>("wgp64x64vd4"), wgp_cfg<2, 2, 4, 0, 3>("wgp64x64d4"),
       wgp_cfg<4, 1, 3, 1, 2>("wgp128x32v"), wgp_cfg<4, 1, 3, 0, 2>("wgp128x32"),
 #ifdef BH_WG_DIAG
-      wg_cfg<2, 2, 3, 1, 4, 1>("xwg64x64v_noxf"), wg_cfg<2, 2, 3, 1, 4, 2>("xwg64x64v_nomfma"),
-      wg_cfg<2, 2, 3, 1, 4, 4>("xwg64x64v_nodma"), wg_cfg<2, 2, 3, 1, 4, 8>("xwg64x64v_nostore"),
-      wg_cfg<2, 2, 3, 1, 4, 7>("xwg64x64v_onlyskel"), wg_cfg<2, 2, 3, 1, 4, 3>("xwg64x64v_noxfmfma"),
+      // diagnostic builds (wrong results by design): one part of the stage dropped each
+      wgp_cfg<4, 1, 3, 0, 2, 1>("xwgp_noxf"), wgp_cfg<4, 1, 3, 0, 2, 2>("xwgp_nomfma"),
+      wgp_cfg<4, 1, 3, 0, 2, 4>("xwgp_nodma"), wgp_cfg<4, 1, 3, 0, 2, 16>("xwgp_nou"),
+      wgp_cfg<4, 1, 3, 0, 2, 32>("xwgp_novf"), wgp_cfg<4, 1, 3, 0, 2, 64>("xwgp_nouwait"),
+      wgp_cfg<4, 1, 3, 0, 2, 7>("xwgp_skel"), wgp_cfg<4, 1, 3, 0, 2, 8>("xwgp_nostore"),
+      wgp_cfg<4, 1, 3, 0, 2, 53>("xwgp_onlymfma"), wgp_cfg<4, 1, 3, 0, 2, 181>("xwgp_onlymfma_nobar"),
 #endif
   };
 }
@@ -1053,7 +633,7 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   if (KY != 3 || KX != 3 || sy != 1 || sx != 1 || py > 1 || px > 1)
     return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for stride-1 3x3 convs with pad <= 1");
   if (IC % WCI) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs IC % 4 == 0");
-  if (c.dc_s && W % 4) return bh::fail(BH_UNSUP, std::string("conv: 16-B strip pieces of ") + c.name + " need W % 4 == 0");
+  if (c.dc_s && W % 4) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for W % 4 == 0 (no row masks)");
   WgArgs p{};
   const uint32_t OH = H + 2 * py - 2, OW = W + 2 * px - 2;
   const uint32_t TH = (OH + 1) / 2, TW = (OW + 1) / 2, TPI = TH * TW;
@@ -1069,8 +649,7 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
     const uint32_t a = gi * TT, b = std::min(T, a + TT) - 1;
     rin = std::max(rin, vrow(b) + 4 - vrow(a));
   }
-  const bool piped = c.dc_wpm != 0;  // wgp: strip-only slots, three V buffers, 16-B pieces always
-  const uint32_t PW = (c.dc_s || piped) ? 4 : 1, SP = (uint32_t)c.dc_rin;
+  const uint32_t PW = 4, SP = (uint32_t)c.dc_rin;  // 16-B strip pieces
   if ((uint64_t)WCI * rin * WPM > (uint64_t)SP * NT * PW)
     return bh::fail(BH_UNSUP, std::string("conv: input strip too large for ") + c.name);
   const uint64_t out_bytes = (uint64_t)B * out_ctot * OH * OW * 4;
@@ -1097,9 +676,9 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   f = bh::make_fastdiv(ipt); p.ipt_m = f.m; p.ipt_s = f.s;
   p.relu = relu;
   p.wt = wt;
-  // dynamic LDS: D slots (U + guard + strip), two V buffers, the ticket flag
-  const uint32_t slot = (piped ? 0 : WCI * OCT * 16) + 4 + SP * NT * PW;
-  const uint32_t lds = (D * slot + (piped ? 3 : 2) * WCI * TT * 16 + 4) * 4;
+  // dynamic LDS: D strip slots (guard + strip), three V buffers, the ticket flag
+  const uint32_t slot = 4 + SP * NT * PW;
+  const uint32_t lds = (D * slot + 3 * WCI * TT * 16 + 4) * 4;
   if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: LDS too small for ") + c.name);
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -86,7 +86,7 @@ def test_wg_rejects_other_shapes(dev, cn):
         dev.tune_set(1, -1, 0)
 
 
-@pytest.mark.parametrize("cn", [n for n in WG if n in ("wg64x64", "wg128x32v")])
+@pytest.mark.parametrize("cn", [n for n in WG if n in ("wgp64x64", "wgp128x32v")])
 def test_wg_residual_and_slab(dev, cn):
     s = ops.ConvShape(2, 32, 28, 28, 96, 3, 3, 1, 1, 1, 1)
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)

@@ -166,7 +166,7 @@ def main():
                         continue
                     if cn.startswith("wg"):  # Winograd 3x3: S = grid mode as stream-K; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 3 and s.sy == s.sx == 1 and s.py <= 1 and s.px <= 1:
-                            cand += [(ci, 1), (ci, 2), (ci, 5), (ci, 11), (ci, 12), (ci, 15)]
+                            cand += [(ci, 1), (ci, 5), (ci, 11), (ci, 15)]  # one block per CU (256 AGPRs)
                         continue
                     if cn.startswith("ks"):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 1 and s.sy == s.sx == 1 and s.py == s.px == 0:
