@@ -59,6 +59,7 @@ struct WgArgs {
   int ocs;                       // tile order: 0 = output-channel tile fastest, 1 = slowest
   uint32_t ipt, ipt_m, ipt_s, ipb, total_it;
   int relu, wt;
+  int ow2;                       // OW even: a tile row's two outputs go as one 8-B store
 #ifdef BH_KTRACE
   unsigned long long *trace;
 #endif
@@ -118,7 +119,7 @@ __device__ __forceinline__ void wg_store1(const WgArgs &p, __amdgpu_buffer_rsrc_
 //  * V is triple-buffered: stage it+2's patches are transformed during stage it, so stage it+1's V
 //    is complete at the top of stage it and its fragments load under stage it's MFMAs;
 //  * the strip ring (LDS-DMA) holds stages it+2 .. it+D+1: each strip has two stages to land.
-template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
+template <int NWO, int NWT, int D, int V4, int SP, int IL, int DBG = 0>
 __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT;
   constexpr int PW = 4;                       // floats per strip piece (16 B; rows of W % 4 != 0 run
@@ -327,6 +328,56 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     }
   };
 
+  // IL: the same transform in eight slices, one between each pair of MFMAs of the stage (a VALU /
+  // LDS instruction issued while an MFMA runs costs no issue time; a run of them between MFMA groups
+  // does)
+  float tq[4][4];
+  auto tx_part = [&](int vb, int part) {
+    float *const vd = vbase + vb * VSZ + (xcl * TT + xtt) * 16;
+    const uint32_t r2 = (xtt >> 2) & 3u;
+    auto put = [&](uint32_t x, const float (&t)[4]) {
+      const f32x4v v = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+      *(f32x4v *)(vd + ((x + r2) & 3u) * 4) = v;
+    };
+    if constexpr (TS == 1) {
+      if (part < 2) {
+        if constexpr (!V4) {
+#pragma unroll
+          for (int r = 2 * part; r < 2 * part + 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[r][c] = (xm >> c) & 1u ? d[r][c] : 0.0f;
+        }
+      } else if (part < 4) {
+#pragma unroll
+        for (int c = 2 * (part - 2); c < 2 * (part - 2) + 2; ++c) {
+          tq[0][c] = d[0][c] - d[2][c];
+          tq[1][c] = d[1][c] + d[2][c];
+          tq[2][c] = d[2][c] - d[1][c];
+          tq[3][c] = d[1][c] - d[3][c];
+        }
+      } else {
+        put((uint32_t)(part - 4), tq[part - 4]);
+      }
+    } else {
+      if (part < 3) {
+        if constexpr (!V4) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) d[part][c] = (xm >> c) & 1u ? d[part][c] : 0.0f;
+        }
+      } else if (part == 3) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          tq[0][c] = xh ? d[1][c] - d[0][c] : d[0][c] - d[2][c];
+          tq[1][c] = xh ? d[0][c] - d[2][c] : d[1][c] + d[2][c];
+        }
+      } else if (part == 4) {
+        put(2 * xh, tq[0]);
+      } else if (part == 5) {
+        put(2 * xh + 1, tq[1]);
+      }
+    }
+  };
+
   // ---- V fragments (buffer vb), group g: tile wtl*32 + li, channel 2s + kh; one register buffer
   // like U
   f32x4v vf[2][4];
@@ -383,6 +434,27 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     const uint32_t oc = oc0 + (uint32_t)(wo * 32 + 8 * (q >> 2) + 4 * kh + (q & 3));
     const bool ok = stv & (oc < p.OC);
     const uint32_t o = sob + oc * p.OHW;
+    if (p.ow2) {  // uniform; o even, so both 8-B pieces are aligned (every tile has both columns)
+      const uint32_t off[2] = {oob_unless(ok, o * 4u), oob_unless(ok & sy1, (o + p.OW) * 4u)};
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float z0 = yy[2 * e] + bias[q], z1 = yy[2 * e + 1] + bias[q];
+        if (p.res) {  // (two dword loads: hipcc lowered an 8-B raw_buffer_load here to a 4-B one)
+          z0 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
+          z1 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 4, 0));
+        }
+        if (p.relu) {
+          z0 = z0 < 0.0f ? 0.0f : z0;
+          z1 = z1 < 0.0f ? 0.0f : z1;
+        }
+        const __attribute__((ext_vector_type(2))) uint32_t v = {__builtin_bit_cast(uint32_t, z0),
+                                                               __builtin_bit_cast(uint32_t, z1)};
+        const uint32_t oo = (DBG & 8) ? OOB : off[e];
+        if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, oo, 0, AUX_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b64(v, rso, oo, 0, AUX_OUT);
+      }
+      return;
+    }
     const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1, (o + 1) * 4u),
                              oob_unless(ok & sy1, (o + p.OW) * 4u), oob_unless(ok & sx1 & sy1, (o + p.OW + 1) * 4u)};
 #pragma unroll
@@ -515,6 +587,44 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     const uint32_t su = plan_u(it + 1);
     __builtin_amdgcn_sched_barrier(0);
     constexpr int QG = (SP + 3) / 4;
+    if constexpr (IL) {
+      auto mf = [&](int st, int x, int n) {
+        acc[4 * x + n] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[st][x][n], vf[st][x][n], acc[4 * x + n], 0, 0, 0);
+      };
+      auto chunk = [&](int st, int x) {  // stage it+1's U and V fragments of chunk x, k step st
+        ur[st][x] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[st][x], su, 0));
+        vf[st][x] = *(const f32x4v *)(vbase + vb1 * VSZ + ((2 * st + kh) * TT + wtl * 32 + li) * 16 + co[x]);
+      };
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int st = x >> 1, c0 = 2 * (x & 1), c1 = c0 + 1;
+        vm_wait<6 + SP>();  // U(it) group x landed
+        mf(st, c0, 0);
+        mf(st, c0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        tx_part(vb2, 2 * x);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(st, c0, 2);
+        mf(st, c0, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        chunk(st, c0);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(st, c1, 0);
+        mf(st, c1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        tx_part(vb2, 2 * x + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(st, c1, 2);
+        mf(st, c1, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        chunk(st, c1);
+#pragma unroll
+        for (int j = x * QG; j < (x + 1) * QG; ++j) {
+          if (j < SP) issue_strip(j, sl1, ss, dead);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       if constexpr ((DBG & 64) == 0) vm_wait<6 + SP>();  // U(it) group x landed
@@ -534,6 +644,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
         if constexpr ((DBG & 1) == 0) tx_write(vb2);
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
     }
 #ifdef BH_KTRACE
     { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); tk[4] += tn_ - tkp; tkp = tn_; }
@@ -578,10 +689,10 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
 #endif
 }
 
-template <int NWO, int NWT, int D, int V4, int SP, int DBG = 0>
+template <int NWO, int NWT, int D, int V4, int SP, int IL, int DBG = 0>
 cfg_t wgp_cfg(const char *name) {
   cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgp_kernel<NWO, NWT, D, V4, SP, DBG>;
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgp_kernel<NWO, NWT, D, V4, SP, IL, DBG>;
   c.dc = 4;
   c.dc_ky = 3;
   c.dc_kx = 3;
@@ -597,16 +708,20 @@ std::vector<cfg_t> wg_cfgs() {
   // <NWO, NWT, D, V4, SP>: OCT = 32 NWO channels x TT = 32 NWT tiles; D strip slots; V4: W % 4 == 0
   // (no row masks); SP strip DMA pieces per thread and stage
   return {
-      wgp_cfg<2, 2, 3, 1, 4>("wgp64x64v"), wgp_cfg<2, 2, 3, 0, 3>("wgp64x64"),
-      wgp_cfg<2, 2, 4, 1, 3>("wgp64x64vd4"), wgp_cfg<2, 2, 4, 0, 3>("wgp64x64d4"),
-      wgp_cfg<4, 1, 3, 1, 2>("wgp128x32v"), wgp_cfg<4, 1, 3, 0, 2>("wgp128x32"),
+      wgp_cfg<2, 2, 3, 1, 4, 0>("wgp64x64v"), wgp_cfg<2, 2, 3, 0, 3, 0>("wgp64x64"),
+      wgp_cfg<2, 2, 4, 1, 3, 0>("wgp64x64vd4"), wgp_cfg<2, 2, 4, 0, 3, 0>("wgp64x64d4"),
+      wgp_cfg<4, 1, 3, 1, 2, 0>("wgp128x32v"), wgp_cfg<4, 1, 3, 0, 2, 0>("wgp128x32"),
+      // IL: the stage's loads and transform interleaved with its MFMAs
+      wgp_cfg<2, 2, 3, 1, 4, 1>("wgi64x64v"), wgp_cfg<2, 2, 3, 0, 3, 1>("wgi64x64"),
+      wgp_cfg<2, 2, 4, 1, 3, 1>("wgi64x64vd4"), wgp_cfg<2, 2, 4, 0, 3, 1>("wgi64x64d4"),
+      wgp_cfg<4, 1, 3, 1, 2, 1>("wgi128x32v"), wgp_cfg<4, 1, 3, 0, 2, 1>("wgi128x32"),
 #ifdef BH_WG_DIAG
       // diagnostic builds (wrong results by design): one part of the stage dropped each
-      wgp_cfg<4, 1, 3, 0, 2, 1>("xwgp_noxf"), wgp_cfg<4, 1, 3, 0, 2, 2>("xwgp_nomfma"),
-      wgp_cfg<4, 1, 3, 0, 2, 4>("xwgp_nodma"), wgp_cfg<4, 1, 3, 0, 2, 16>("xwgp_nou"),
-      wgp_cfg<4, 1, 3, 0, 2, 32>("xwgp_novf"), wgp_cfg<4, 1, 3, 0, 2, 64>("xwgp_nouwait"),
-      wgp_cfg<4, 1, 3, 0, 2, 7>("xwgp_skel"), wgp_cfg<4, 1, 3, 0, 2, 8>("xwgp_nostore"),
-      wgp_cfg<4, 1, 3, 0, 2, 53>("xwgp_onlymfma"), wgp_cfg<4, 1, 3, 0, 2, 181>("xwgp_onlymfma_nobar"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 1>("xwgp_noxf"), wgp_cfg<4, 1, 3, 0, 2, 0, 2>("xwgp_nomfma"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 4>("xwgp_nodma"), wgp_cfg<4, 1, 3, 0, 2, 0, 16>("xwgp_nou"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 32>("xwgp_novf"), wgp_cfg<4, 1, 3, 0, 2, 0, 64>("xwgp_nouwait"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 7>("xwgp_skel"), wgp_cfg<4, 1, 3, 0, 2, 0, 8>("xwgp_nostore"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 53>("xwgp_onlymfma"), wgp_cfg<4, 1, 3, 0, 2, 0, 181>("xwgp_onlymfma_nobar"),
 #endif
   };
 }
@@ -676,6 +791,7 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   f = bh::make_fastdiv(ipt); p.ipt_m = f.m; p.ipt_s = f.s;
   p.relu = relu;
   p.wt = wt;
+  p.ow2 = OW % 2 == 0 ? 1 : 0;
   // dynamic LDS: D strip slots (guard + strip), three V buffers, the ticket flag
   const uint32_t slot = 4 + SP * NT * PW;
   const uint32_t lds = (D * slot + 3 * WCI * TT * 16 + 4) * 4;
