@@ -261,6 +261,11 @@ def main():
                       "roofline_ms": round(rt * 1e3, 4),
                       # the reference's own per-call convention (event pair around each call)
                       "sum_event_ms": round(te * 1e3, 4), "roofline_frac_events": round(rt / te, 4)}
+        # ops on the Winograd route (fewer MFMA flops than the direct flop model the roofline
+        # counts): their count and time
+        wr = [r for r in rs if "_wino_" in r.get("variant", "")]
+        if wr:
+            per_set[n].update({"wino_ops": len(wr), "wino_kernel_ms": round(sum(r["kernel_s"] for r in wr) * 1e3, 4)})
         if all(r["vendor_s"] is not None for r in rs):
             tv = sum(r["vendor_s"] for r in rs)
             per_set[n].update({"vendor_ms": round(tv * 1e3, 4), "vendor_roofline_frac": round(rt / tv, 4),

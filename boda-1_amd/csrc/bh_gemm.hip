@@ -1080,7 +1080,7 @@ std::string describe_cfg(int op, const uint32_t *d, choice_t const &ch) {
   if (c.streamk) return s + "_streamk";
   if (c.dc == 2) return std::string("mfma32_conv_dm_") + c.name;
   if (c.dc == 3) return std::string("mfma32_conv_k1s_") + c.name;
-  if (c.dc == 4) return std::string("mfma16_conv_wino_") + c.name;
+  if (c.dc == 4) return std::string("mfma32_conv_wino_") + c.name;
   if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
   if (c.fcv) return std::string("conv_fcv_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
