@@ -191,6 +191,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
       uint32_t oc0, g0, v0;
       int x0;
       tile_of(t, oc0, g0);
+      if constexpr ((DBG & 512) != 0) g0 = 0;  // diagnostic: every tile DMAs tile group 0's strip
       tpos(g0 < p.T ? g0 : 0u, v0, x0);
 #pragma unroll
       for (int j = 0; j < SP; ++j) {  // piece: channel c, row s, column col of the [4][RIN][WPM] image
@@ -224,6 +225,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     if (t != lu_tile) {  // uniform
       uint32_t oc0, g0;
       tile_of(t, oc0, g0);
+      if constexpr ((DBG & 256) != 0) oc0 = 0;  // diagnostic: every tile reads OC tile 0's U (L2-resident)
       const uint32_t oc = oc0 + (uint32_t)(wo * 32 + li);
 #pragma unroll
       for (int st = 0; st < 2; ++st)
@@ -721,6 +723,8 @@ std::vector<cfg_t> wg_cfgs() {
       wgp_cfg<4, 1, 3, 0, 2, 0, 4>("xwgp_nodma"), wgp_cfg<4, 1, 3, 0, 2, 0, 16>("xwgp_nou"),
       wgp_cfg<4, 1, 3, 0, 2, 0, 32>("xwgp_novf"), wgp_cfg<4, 1, 3, 0, 2, 0, 64>("xwgp_nouwait"),
       wgp_cfg<4, 1, 3, 0, 2, 0, 7>("xwgp_skel"), wgp_cfg<4, 1, 3, 0, 2, 0, 8>("xwgp_nostore"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 256>("xwgp_ul2"), wgp_cfg<4, 1, 3, 0, 2, 0, 512>("xwgp_sl2"),
+      wgp_cfg<4, 1, 3, 0, 2, 0, 768>("xwgp_usl2"),
       wgp_cfg<4, 1, 3, 0, 2, 0, 53>("xwgp_onlymfma"), wgp_cfg<4, 1, 3, 0, 2, 0, 181>("xwgp_onlymfma_nobar"),
 #endif
   };
