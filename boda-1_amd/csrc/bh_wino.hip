@@ -795,7 +795,8 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   f = bh::make_fastdiv(ipt); p.ipt_m = f.m; p.ipt_s = f.s;
   p.relu = relu;
   p.wt = wt;
-  p.ow2 = OW % 2 == 0 ? 1 : 0;
+  // 8-B stores need an 8-B aligned output (and residual): callers may pass any float offset
+  p.ow2 = (OW % 2 == 0 && ((uintptr_t)out & 7) == 0 && ((uintptr_t)res & 7) == 0) ? 1 : 0;
   // dynamic LDS: D strip slots (guard + strip), three V buffers, the ticket flag
   const uint32_t slot = 4 + SP * NT * PW;
   const uint32_t lds = (D * slot + 3 * WCI * TT * 16 + 4) * 4;

@@ -115,3 +115,28 @@ def test_wg_residual_and_slab(dev, cn):
             x.free()
     finally:
         dev.tune_set(1, -1, 0)
+
+
+@pytest.mark.parametrize("cn", [n for n in WG if n in ("wgp64x64v", "wgi128x32")])
+def test_wg_dword_aligned_pointers(dev, cn):
+    """Input and output pointers one float past a 16-B boundary (a caller's sub-buffer): the strip
+    DMA takes any dword alignment, and the 8-B paired output stores fall back to dword stores."""
+    s = ops.ConvShape(2, 32, 28, 28, 96, 3, 3, 1, 1, 1, 1)
+    ni, no = s.B * s.IC * s.H * s.W, s.B * s.OC * s.OH * s.OW
+    bi, bo = dev.alloc_floats(ni + 4), dev.alloc_floats(no + 4)
+    f, b = dev.alloc_floats(s.OC * s.K), dev.alloc_floats(s.OC)
+    vi, vo = boda_hip.DevBuf(dev, bi.ptr + 4, ni * 4), boda_hip.DevBuf(dev, bo.ptr + 4, no * 4)
+    dev.gen_data(GEN_CONV_IN, vi, [s.B, s.IC, s.H, s.W], 5)
+    dev.gen_data(GEN_CONV_FILTS, f, [s.OC, s.IC, s.KY, s.KX], 5)
+    dev.gen_data(GEN_CONV_BIASES, b, [s.OC], 5)
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
+    try:
+        dev.conv(vi, f, b, vo, s, 1)
+        got = vo.download()
+        ref = run_conv(dev, s)  # the same configuration on aligned buffers
+    finally:
+        dev.tune_set(1, -1, 0)
+    check(got, s)
+    np.testing.assert_array_equal(got, ref)
+    for x in (bi, bo, f, b):
+        x.free()
