@@ -375,6 +375,13 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 1>("dc11s4x32d2v"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3, 1>("dc11s4x32d3v"),
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2, 1>("dc11s4x96d2v"),
+      // op_sigs' wide stems: 3 x 516^2 -> 96 11x11 s4 and 6x6 s2, 3 x 224^2 -> 96 11x11 s2
+      dc_cfg<11, 11, 4, 516, 19, 1, 1, 2, 1>("dc11s4x32w516d2v"),
+      dc_cfg<6, 6, 2, 516, 10, 1, 1, 3, 1>("dc6s2x32w516d3v"),
+      dc_cfg<6, 6, 2, 516, 10, 3, 1, 2, 1>("dc6s2x96w516d2v"),
+      dc_cfg<6, 6, 2, 516, 10, 2, 2, 2, 1>("dc6s2x64n256w516d2v"),
+      dc_cfg<11, 11, 2, 228, 15, 1, 1, 2, 1>("dc11s2x32d2v"),
+      dc_cfg<11, 11, 2, 228, 15, 3, 1, 2, 1>("dc11s2x96d2v"),
       // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
       dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
       dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),

@@ -34,7 +34,16 @@ SHAPES = {
               ops.ConvShape(1, 3, 224, 224, 96, 11, 11, 4, 4, 0, 0),
               ops.ConvShape(2, 2, 60, 71, 40, 11, 11, 4, 4, 2, 1),
               ops.ConvShape(1, 4, 120, 100, 100, 11, 11, 4, 4, 5, 5),
-              ops.ConvShape(1, 4, 100, 224, 40, 11, 11, 4, 4, 1, 1)],  # W % 4 == 0, pad 1 (16-B strip)
+              ops.ConvShape(1, 4, 100, 224, 40, 11, 11, 4, 4, 1, 1),  # W % 4 == 0, pad 1 (16-B strip)
+              ops.ConvShape(1, 3, 100, 516, 96, 11, 11, 4, 4, 0, 0),  # op_sigs' 516-wide stem rows
+              ops.ConvShape(2, 2, 60, 300, 20, 11, 11, 4, 4, 2, 2)],
+    (6, 2): [ops.ConvShape(1, 3, 100, 516, 40, 6, 6, 2, 2, 0, 0),    # op_sigs' 516-wide 6x6 s2 stem rows
+             ops.ConvShape(2, 2, 64, 132, 20, 6, 6, 2, 2, 1, 1),     # 3-row pixel tiles, pad 1
+             ops.ConvShape(1, 4, 40, 60, 33, 6, 6, 2, 2, 0, 2),
+             ops.ConvShape(2, 3, 40, 508, 16, 6, 6, 2, 2, 1, 1)],    # 256-pixel tiles within two rows
+    (11, 2): [ops.ConvShape(1, 3, 224, 224, 96, 11, 11, 2, 2, 0, 0),  # op_sigs' 11x11 s2 stem
+              ops.ConvShape(1, 2, 60, 224, 24, 11, 11, 2, 2, 1, 1),
+              ops.ConvShape(2, 3, 40, 100, 50, 11, 11, 2, 2, 3, 3)],
     (3, 1): [ops.ConvShape(1, 3, 224, 224, 64, 3, 3, 1, 1, 1, 1),
              ops.ConvShape(2, 3, 50, 210, 20, 3, 3, 1, 1, 1, 1),
              ops.ConvShape(1, 2, 40, 200, 70, 3, 3, 1, 1, 0, 2)],
