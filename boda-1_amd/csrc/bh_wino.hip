@@ -67,6 +67,9 @@ struct WgArgs {
 
 namespace {
 
+#ifndef WG_QP
+#define WG_QP 4
+#endif
 constexpr int WCI = 4;  // input channels per stage (two k-steps of 32x32x2 MFMAs)
 
 // Filter transform: u[ic][oc][chunk rotated] = G g G^T for oc < OC32, ic < IC4 (zero past OC / IC)
@@ -499,24 +502,28 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     if (!*flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
     const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+    // QP accumulator elements per pass: each slab's QP loads go out together, so a pass waits one
+    // memory latency per slab (with 4 per pass the last arriver of a tile cut into ~11 pieces
+    // spent about as long in this loop as the whole tile's stages, tools/wg_phases.py at batch 5)
+    constexpr int QP = WG_QP;
 #pragma unroll
-    for (int q0 = 0; q0 < NQ; q0 += 4) {
-      f32x4v y[4];
+    for (int q0 = 0; q0 < NQ; q0 += QP) {
+      f32x4v y[QP];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int i = 0; i < QP; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       for (uint32_t b = b0; b <= b1; ++b) {  // block order = k order: bitwise reproducible
         const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
         const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
-        f32x4v x[4];
+        f32x4v x[QP];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < QP; ++i)
           x[i] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
                                                 rall, base + (uint32_t)(((q0 + i) * NT + tid) * 16), 0, AUX_SC1));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] += x[i];
+        for (int i = 0; i < QP; ++i) y[i] += x[i];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) store_q(oc0, q0 + i, y[i]);
+      for (int i = 0; i < QP; ++i) store_q(oc0, q0 + i, y[i]);
     }
   };
 

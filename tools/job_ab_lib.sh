@@ -8,7 +8,7 @@ for d in ${WG_OPS:-20,64,56,56,192 20,384,13,13,384 20,144,14,14,288 20,128,28,2
   OPS+=(--conv "$d,3,3,1,1,1,1")
 done
 tools/gpu_job.sh \
-  a1 200 env BH_LIB_NAME=libboda_hip.so python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits 11,15 --json gpurun_out/ab_a1.json :: \
-  b1 200 env BH_LIB_NAME=$AB_LIB python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits 11,15 --json gpurun_out/ab_b1.json :: \
-  a2 200 env BH_LIB_NAME=libboda_hip.so python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits 11,15 --json gpurun_out/ab_a2.json :: \
-  b2 200 env BH_LIB_NAME=$AB_LIB python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits 11,15 --json gpurun_out/ab_b2.json
+  a1 200 env BH_LIB_NAME=${AB_BASE:-libboda_hip.so} python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits ${SPLITS:-11,15} --json gpurun_out/ab_a1.json :: \
+  b1 200 env BH_LIB_NAME=$AB_LIB python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits ${SPLITS:-11,15} --json gpurun_out/ab_b1.json :: \
+  a2 200 env BH_LIB_NAME=${AB_BASE:-libboda_hip.so} python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits ${SPLITS:-11,15} --json gpurun_out/ab_a2.json :: \
+  b2 200 env BH_LIB_NAME=$AB_LIB python -u tools/cfgprobe.py "${OPS[@]}" --cfg wg --splits ${SPLITS:-11,15} --json gpurun_out/ab_b2.json
