@@ -68,7 +68,7 @@ struct WgArgs {
 namespace {
 
 #ifndef WG_QP
-#define WG_QP 4
+#define WG_QP 8
 #endif
 constexpr int WCI = 4;  // input channels per stage (two k-steps of 32x32x2 MFMAs)
 
