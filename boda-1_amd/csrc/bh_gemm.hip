@@ -1235,8 +1235,10 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   if (cfgs(1)[ch.cfg].packA) {
     // ring kernels read the filter bank k-major: repack it first (this call's first dispatch)
     // (K order (ky, kx, ic), rows padded to a multiple of 64; input offsets + 2^30 must miss)
+    // pk_floats (the whole pack: k-major bank + the Winograd U bank of a 3x3) sizes the buffer and
+    // the 2 GiB check; the k-major kernels see only the k-major part, so reads past it are misses
     const size_t pk_floats = conv_filts_packed_floats(OC, IC, KY, KX);
-    const uint32_t oc4 = (OC + 3) & ~3u, kp = (uint32_t)(pk_floats / oc4);
+    const uint32_t oc4 = (OC + 3) & ~3u, kp = (uint32_t)(kmajor_floats(OC, IC, KY, KX) / oc4);
     const float *wp = packed;
     if (pk_floats * 4 >= 0x7fffffc0ull || in_bytes >= (1ull << 30)) {
       ch = heuristic(1, d, false);

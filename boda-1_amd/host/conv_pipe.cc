@@ -256,8 +256,12 @@ p_conv_pipe_t create_pipe_from_prototxt(std::string const &text, uint32_t img, s
       // mode's deterministic mask (an in-place op, src/rtc_fwd.cc:348-358)
       p_pt_msg p = lp->sub("dropout_param");
       op->dropout_ratio = p ? f32(p->get("dropout_ratio", "0.5"), "dropout_ratio") : 0.5f;
-      if (op->tops != op->bots) op->type = "Copy";
-      else if (!det_dropout) { keep = false; why = "Dropout in place (identity at test time)"; }
+      if (op->tops != op->bots) {
+        // the rtc mode's dropout is an in-place op (src/rtc_fwd.cc:349 asserts it); the TEST-phase
+        // identity of an out-of-place one is a copy, which is only right without det_dropout
+        if (det_dropout) rt_err("layer '" + op->tag + "': det_dropout needs an in-place Dropout");
+        op->type = "Copy";
+      } else if (!det_dropout) { keep = false; why = "Dropout in place (identity at test time)"; }
     } else if (op->type == "Data") {
       p_pt_msg tp = lp->sub("transform_param"), dp = lp->sub("data_param");
       if (!tp || !dp) rt_err("Data layer '" + op->tag + "' without transform_param / data_param");
@@ -829,7 +833,7 @@ void conv_pipe_fwd_t::run_fwd(vect_string const &to_set_vns, p_map_str_p_nda_t c
     layer_time_t t;
     t.tag = calls[i].tag;
     t.func = calls[i].rfc.rtc_func_name;
-    t.ms = enable_prof ? rtc->get_dur(ids[i], ids[i]) : 0.0;
+    t.ms = rtc->get_dur(ids[i], ids[i]);  // every call has its event pair (src/rtc_fwd.cc:563)
     t.flops = calls[i].flops;
     times.push_back(t);
   }
@@ -841,6 +845,8 @@ void conv_pipe_fwd_t::run_fwd(vect_string const &to_set_vns, p_map_str_p_nda_t c
     for (auto const &t : times)
       fprintf(f, "per_layer_time['%s']=per_layer_time.get('%s',0.0) + %.9g # %s \n", t.tag.c_str(), t.tag.c_str(),
               t.ms / 1000.0, t.func.c_str());
+    // (the reference also appends cp->dump_ops, its op-graph dump, src/rtc_fwd.cc:568: this
+    // backend's equivalent is boda_hip_rtc_fwd --plan-exec, not written here)
     fclose(f);
   }
   stats_map.clear();

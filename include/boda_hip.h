@@ -38,7 +38,7 @@ extern "C" {
 #define BH_ERR 1
 #define BH_UNSUP 2
 
-#define BH_ABI_VERSION 1
+#define BH_ABI_VERSION 2
 
 typedef struct bh_ctx bh_ctx;
 
@@ -142,9 +142,13 @@ int bh_conv2d_fwd_nchw(bh_ctx *ctx, const float *in, const float *filts, const f
 /* Filter-bank transform for the conv variants that read the filters k-major --
  * Boda's xpose_filts (test/rtc/xpose_filts.cucl, run once per var before the
  * timed calls: src/rtc_prof.cc:93-99, src/rtc_fwd.cc:306-326). packed receives
- * bh_conv_filts_packed_floats(OC, IC, KY, KX) floats: row (ky*KX+kx)*IC + ic holds
- * filts[*][ic][ky][kx] for every output channel (rows padded to a multiple of 4
- * floats, zero rows up to a multiple of 64). */
+ * bh_conv_filts_packed_floats(OC, IC, KY, KX) floats:
+ *  - the k-major bank: row (ky*KX+kx)*IC + ic holds filts[*][ic][ky][kx] for every
+ *    output channel (rows padded to a multiple of 4 floats, zero rows up to a
+ *    multiple of 64);
+ *  - ABI 2: for KY == KX == 3 only, followed by the Winograd F(2x2,3x3) bank U =
+ *    G g G^T, [ceil4(IC)][ceil32(OC)][16] floats (each (ic, oc) row's four 4-float
+ *    chunks rotated by (oc >> 2) & 3), about 1.8x the k-major bank's size. */
 size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int bh_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC,
                        uint32_t KY, uint32_t KX);

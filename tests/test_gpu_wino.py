@@ -6,7 +6,8 @@ shapes whose tiles run across tile rows and images (odd 13x13 / 7x7 outputs with
 tile row and column, 6x6, 14x14, 28x28, 56x56), ragged output channels (not a multiple of the 64- /
 128-channel tile, nor of 32), unpadded and non-square inputs, under every grid mode the tuner may
 pick (splits 0: stream-K at the occupancy's blocks per CU, 1 / 2 blocks per CU, 5: whole tiles per
-block). The result is an exact-fp32 Winograd sum, so it is checked against the double-accumulated
+block; 11 / 15: the same with the OC tile slowest -- the ngr fastdiv branch of tile_of and another
+stream-K slab / ticket pattern). The result is an exact-fp32 Winograd sum, so it is checked against the double-accumulated
 oracle with the tolerances of test_gpu_conv.py -- the same bar every direct route
 meets (the reference widens its own compare to 2e-3 for cuDNN's 3x3 Winograd,
 src/rtc_prof.cc:314-319; this one does not need it). A rerun gives the same bits (cut tiles are
@@ -54,7 +55,7 @@ def test_wg_config(dev, cn):
     ran = 0
     try:
         for s in SHAPES:
-            for splits in (0, 1, 2, 5):
+            for splits in (0, 1, 2, 5, 11, 15):
                 dev.tune_set(1, ci, splits)
                 try:
                     out = run_conv(dev, s)

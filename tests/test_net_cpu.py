@@ -138,3 +138,20 @@ def test_det_dropout_plan():
     assert [o["tag"] for o in drops] == ["drop6", "drop7"] and all(o["ratio"] == 0.5 for o in drops)
     assert all(o["tops"] == o["bots"] for o in drops)
     assert "drop6" not in " ".join(p1["ignored"])
+
+
+def test_det_dropout_needs_in_place(tmp_path):
+    """The rtc mode's Dropout is an in-place op (src/rtc_fwd.cc:349 asserts it): under --det-dropout
+    an out-of-place Dropout is an error, not a silent copy; without it, the TEST-phase identity of
+    an out-of-place Dropout is a Copy."""
+    pt = tmp_path / "drop.prototxt"
+    pt.write_text('name: "d"\ninput: "data"\ninput_dim: 1\ninput_dim: 8\ninput_dim: 4\ninput_dim: 4\n'
+                  'layer { name: "drop" type: "Dropout" bottom: "data" top: "y" '
+                  'dropout_param { dropout_ratio: 0.5 } }\n')
+    r = subprocess.run([BIN, "--net", str(pt), "--img", "1", "--plan-json", "--det-dropout", "5"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "in-place Dropout" in r.stderr, (r.returncode, r.stderr)
+    r = subprocess.run([BIN, "--net", str(pt), "--img", "1", "--plan-json"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert [o["type"] for o in json.loads(r.stdout)["ops"]] == ["Copy"]
