@@ -99,13 +99,16 @@ def cpu_info():
 
 
 def executed_flops(s, variant):
-    """Flops an op's kernel actually issues: the Winograd F(2x2, 3x3) route multiplies 16 transformed
-    input values by 16 transformed filter values per 2x2 output tile and (input, output) channel pair
-    (odd outputs computed to the next even size), the other routes the direct-form 2*M*N*K of
-    src/latex-util.H:116-120 (SGEMM: 2*M*N*K)."""
+    """Flops an op's kernel actually issues: a Winograd route multiplies its transformed input values by
+    the transformed filter values position by position, per output tile and (input, output) channel
+    pair (outputs computed up to a whole number of tiles), the other routes the direct-form 2*M*N*K
+    of src/latex-util.H:116-120 (SGEMM: 2*M*N*K)."""
     if "_wino_" in variant:
-        tiles = s.B * ((s.OH + 1) // 2) * ((s.OW + 1) // 2)
-        return 2.0 * 16 * s.OC * s.IC * tiles
+        # wx43: F(4x4, 3x3), 36 products per 4x4 tile; wx25: F(2x2, 5x5), 36 per 2x2 tile; wg* / wx23:
+        # F(2x2, 3x3), 16 per 2x2 tile
+        mo, pos = (4, 36) if "_wino_wx43" in variant else ((2, 36) if "_wino_wx25" in variant else (2, 16))
+        tiles = s.B * (-(-s.OH // mo)) * (-(-s.OW // mo))
+        return 2.0 * pos * s.OC * s.IC * tiles
     return s.flops()
 
 

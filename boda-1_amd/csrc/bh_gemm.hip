@@ -760,6 +760,7 @@ std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
     for (auto const &c : dcm_cfgs()) v.push_back(c);
     for (auto const &c : k1s_cfgs()) v.push_back(c);
     for (auto const &c : wg_cfgs()) v.push_back(c);
+    for (auto const &c : wgx_cfgs()) v.push_back(c);
   }
   return v;
 }
@@ -1080,7 +1081,7 @@ std::string describe_cfg(int op, const uint32_t *d, choice_t const &ch) {
   if (c.streamk) return s + "_streamk";
   if (c.dc == 2) return std::string("mfma32_conv_dm_") + c.name;
   if (c.dc == 3) return std::string("mfma32_conv_k1s_") + c.name;
-  if (c.dc == 4) return std::string("mfma32_conv_wino_") + c.name;
+  if (c.dc == 4 || c.dc == 5) return std::string("mfma32_conv_wino_") + c.name;
   if (c.dc) return std::string("mfma32_conv_direct_") + c.name;
   if (c.fcv) return std::string("conv_fcv_") + c.name;
   if (c.gv) return std::string("mfma16_conv_gv_") + c.name;
@@ -1244,12 +1245,12 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
       ch = heuristic(1, d, false);
     } else {
       bool rp = repacked;  // a repack of this call already dispatched (it recorded the start event)
-      const bool wino = cfgs(1)[ch.cfg].dc == 4;  // reads the Winograd part of a 3x3 pack
+      const bool wino = cfgs(1)[ch.cfg].dc == 4 || cfgs(1)[ch.cfg].dc == 5;  // reads a Winograd part of the pack
       if (!wp) {
         int rc = ensure_wpack(ctx, pk_floats * 4);
-        if (rc == BH_OK) rc = launch_xpose_filts(ctx, filts, (float *)ctx->wpack, OC, IC, KY * KX, first, false);
-        if (rc == BH_OK && wino && KY == 3 && KX == 3)
-          rc = launch_wino_pack(ctx, filts, (float *)ctx->wpack + kmajor_floats(OC, IC, KY, KX), OC, IC, false, false);
+        if (rc == BH_OK)
+          rc = wino ? launch_pack_all(ctx, filts, (float *)ctx->wpack, OC, IC, KY, KX, first, false)
+                    : launch_xpose_filts(ctx, filts, (float *)ctx->wpack, OC, IC, KY * KX, first, false);
         if (rc != BH_OK) return rc;
         wp = (const float *)ctx->wpack;
         rp = true;
@@ -1269,6 +1270,11 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
                                                         out_ctot, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, p.wt,
                                                         ch.splits, kfirst)
                                             : bh::fail(BH_UNSUP, std::string("conv: ") + dcc.name + " is for 3x3 convs"))
+                       : dcc.dc == 5 ? (wino_bank_offset(OC, IC, KY, KX, (uint32_t)dcc.dc_s) && KY == (uint32_t)dcc.dc_ky
+                                            ? launch_wgx(ctx, dcc, wp + wino_bank_offset(OC, IC, KY, KX, (uint32_t)dcc.dc_s),
+                                                         in, biases, res, out, out_ctot, B, IC, H, W, OC, KY, KX, sy, sx,
+                                                         py, px, relu, p.wt, ch.splits, kfirst)
+                                            : bh::fail(BH_UNSUP, std::string("conv: ") + dcc.name + " is for other kernel sizes"))
                                      : launch_dc(ctx, dcc, p, B, KY, KX, sy, sx, kfirst);
         if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
         return launch_conv(ctx, in, filts, wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, out_ctot,

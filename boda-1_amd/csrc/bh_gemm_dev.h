@@ -388,6 +388,22 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
               uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
               bool first);
 size_t wino_bank_floats(uint32_t OC, uint32_t IC);
+// bh_wgx.hip: position-split Winograd (F(4x4,3x3), F(2x2,5x5), F(2x2,3x3); two waves per SIMD); u = the
+// bank of the configuration's form (wgx_bank_offset into a pack)
+std::vector<cfg_t> wgx_cfgs();
+int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
+               float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+               uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
+               bool first);
+size_t wx_bank_floats(uint32_t OC, uint32_t IC);
+int launch_wx_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, uint32_t R, bool first,
+                   bool last);
+// every part of a conv pack after the k-major bank: 3x3 -- the F(2x2,3x3) bank, then the F(4x4,3x3)
+// bank; 5x5 -- the F(2x2,5x5) bank. Offsets in floats from the pack's start (0: no such bank)
+size_t pack_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
+size_t wino_bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t MO);
+int launch_pack_all(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX,
+                    bool first, bool last);
 int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, bool first, bool last);
 // floats of the k-major bank (the first part of every pack)
 size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);

@@ -953,6 +953,33 @@ size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
   return (size_t)(((uint64_t)IC * KY * KX + 63) & ~63ull) * ((OC + 3) & ~3u);
 }
 
+size_t pack_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
+  const size_t km = kmajor_floats(OC, IC, KY, KX);
+  if (KY == 3 && KX == 3) return km + wino_bank_floats(OC, IC) + wx_bank_floats(OC, IC);
+  if (KY == 5 && KX == 5) return km + wx_bank_floats(OC, IC);
+  return km;
+}
+
+size_t wino_bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t MO) {
+  const size_t km = kmajor_floats(OC, IC, KY, KX);
+  if (KY == 3 && KX == 3) return MO == 2 ? km : km + wino_bank_floats(OC, IC);
+  if (KY == 5 && KX == 5 && MO == 2) return km;
+  return 0;
+}
+
+// the whole pack: k-major bank, then the Winograd banks of the kernel size (a 3x3's F(2x2,3x3) bank
+// (bh_wino.hip) and F(4x4,3x3) bank, a 5x5's F(2x2,5x5) bank (bh_wgx.hip))
+int launch_pack_all(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX,
+                    bool first, bool last) {
+  const bool w3 = KY == 3 && KX == 3, w5 = KY == 5 && KX == 5;
+  const size_t km = kmajor_floats(OC, IC, KY, KX);
+  int rc = launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, first, last && !w3 && !w5);
+  if (rc == BH_OK && w3) rc = launch_wino_pack(ctx, filts, packed + km, OC, IC, false, false);
+  if (rc == BH_OK && w3) rc = launch_wx_pack(ctx, filts, packed + km + wino_bank_floats(OC, IC), OC, IC, 3, false, last);
+  if (rc == BH_OK && w5) rc = launch_wx_pack(ctx, filts, packed + km, OC, IC, 5, false, last);
+  return rc;
+}
+
 int ensure_wpack(bh_ctx *ctx, size_t bytes) {
   return bh::grow_buffer(ctx, ctx->wpack, ctx->wpack_bytes, bytes, false, "filter-bank pack buffer");
 }
@@ -960,17 +987,13 @@ int ensure_wpack(bh_ctx *ctx, size_t bytes) {
 }  // namespace bhk
 
 namespace bh {
-// the k-major bank, then for 3x3 kernels the Winograd bank U (bh_wino.hip) right behind it
+// the k-major bank, then the Winograd banks of the kernel size (bhk::launch_pack_all)
 size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
-  return bhk::kmajor_floats(OC, IC, KY, KX) + (KY == 3 && KX == 3 ? bhk::wino_bank_floats(OC, IC) : 0);
+  return bhk::pack_floats(OC, IC, KY, KX);
 }
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                            uint32_t KX) {
   if (conv_filts_packed_floats(OC, IC, KY, KX) * 4 >= 0x7fffffc0ull) return fail(BH_UNSUP, "conv_filts_pack: bank larger than 2 GiB");
-  const bool w3 = KY == 3 && KX == 3;
-  int rc = bhk::launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, true, !w3);  // a call of its own
-  if (rc == BH_OK && w3)
-    rc = bhk::launch_wino_pack(ctx, filts, packed + bhk::kmajor_floats(OC, IC, KY, KX), OC, IC, false, true);
-  return rc;
+  return bhk::launch_pack_all(ctx, filts, packed, OC, IC, KY, KX, true, true);  // a call of its own
 }
 }  // namespace bh

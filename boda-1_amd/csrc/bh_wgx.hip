@@ -1,0 +1,657 @@
+// bh_wgx.hip -- Winograd convolutions with the transformed-domain positions split over the waves of a
+// block, two waves per SIMD: F(4x4, 3x3) and F(2x2, 5x5) on 6x6 input patches, and F(2x2, 3x3) on
+// 4x4 patches in the same skeleton.
+//
+// Why a second Winograd kernel (bh_wino.hip's wgp_kernel stays for the shapes the tuner keeps it on):
+//  * wgp gives each wave all 16 positions of F(2x2, 3x3) (256 accumulator registers), so a SIMD runs
+//    ONE wave, and whatever that wave issues besides its MFMAs -- the input transform, the operand
+//    loads, the stage barrier, the tile epilogue -- adds to the stage time nearly serially (its
+//    diagnostic builds); at 6x6 patches (36 positions) one wave cannot even hold a
+//    32x32 tile of every position;
+//  * here a wave owns 32 output channels x 32 tiles x PPG positions (9 of 36, or 8 of 16): 144 / 128
+//    accumulators, so two waves share each SIMD and one wave's MFMAs run while the other waits or
+//    transforms; the 8 waves of a block are NOG channel groups x NPG position groups, all sharing
+//    the block's input strip and transformed input V;
+//  * F(4x4, 3x3) computes 16 outputs from 36 products per channel pair (4x fewer MFMA flops than the
+//    direct form, 1.78x fewer than F(2x2, 3x3)); F(2x2, 5x5) 4 outputs from 36 (2.78x fewer than
+//    direct). Their fp32 transforms lose more precision than F(2x2, 3x3): the launcher refuses
+//    IC > 512 (rel-L2 error grows ~ sqrt(IC); at 512 it is ~4e-6, within the tests' 1e-5).
+//
+//   U = G g G^T (filters, N x N per (oc, ic)), V = B^T d B (input patch), M = sum_ic U . V,
+//   Y = A^T M A (MO x MO outputs); points 0, 1, -1, 2, -2 (and infinity) for the 6x6 forms:
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   A^T (F43) = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1], A^T (F25) = its rows 0, 1
+//   with the last column of row 1 = 1. G is made on the host side of the pack kernel in double.
+//
+// Structure (one fused kernel, nothing of U, V or M goes to HBM; one block per unit of OCT = 32 NOG
+// output channels x TT = 32 Winograd tiles of the flattened (image, tile row, tile column) space):
+//  * U (the pack, untimed like Boda's xpose_filts, src/rtc_prof.cc:93-99) goes from L2 straight into
+//    registers, one stage ahead, group by group after the MFMAs that freed the registers;
+//  * the stage's input strip [4 channels][RIN virtual rows][WPM] (rows img*VH + iy + pad, columns
+//    x + pad: a patch of tile column tx starts at column MO*tx) arrives by dword LDS-DMA, misses
+//    for the padding, so the zeros are exact and no masks are needed; two strip slots: stage it+2's
+//    strip is issued at the top of stage it;
+//  * stage it+1's patches are transformed during stage it into the other V buffer by the 256
+//    threads of waves 0-3 (two per patch, wave-uniform halves: each half makes 3 (2) columns
+//    (rows) of V from the whole patch); V [NPG][4][TT][PS], a position group's PPG values contiguous
+//    per (channel, tile), pitch PS (conflict-free 16-B reads for 8 consecutive lanes);
+//  * at the end of the unit the accumulators go through LDS in rounds: every (channel, tile) pair's
+//    P values meet in one thread, which applies A^T M A, bias, residual and ReLU and stores.
+#include "bh_gemm_dev.h"
+
+namespace bhk {
+
+struct WxArgs {
+  const float *u;    // 6x6: [IC4][OC32][36], positions in (group, slot) order; 4x4: bh_wino.hip's bank
+  const float *in;   // B x IC x H x W
+  float *out;        // image stride OCOHW (channel slabs)
+  const float *bias; // OC or null
+  const float *res;  // laid out like out, or null
+  uint32_t u_bytes, in_bytes, out_bytes;
+  uint32_t OC, OC32, IC, B, H, W, pad, OH, OW, OHW, HW, ICHW, OCOHW;
+  uint32_t TW, TPI, VH, T;    // tiles per tile row / per image, virtual rows per image, tiles in all
+  uint32_t WPM, RW;           // strip pitch, RIN * WPM
+  uint32_t tw_m, tw_s, tpi_m, tpi_s, vh_m, vh_s, wpm_m, wpm_s, rw_m, rw_s;
+  uint32_t ngr, ngr_m, ngr_s; // tile groups (+ fastdiv)
+  uint32_t ipt;               // stages per unit (IC / 4)
+  int relu, wt;
+  int vst;                    // OW % MO == 0 and out / res MO-float aligned: a tile row per store
+};
+
+namespace {
+
+constexpr int XC = 4;    // input channels per stage (two k steps of v_mfma_f32_32x32x2_f32)
+constexpr int XTT = 32;  // tiles per unit
+
+// NW waves per block: 8 (one block per CU, two waves per SIMD) or 4 (two blocks per CU)
+template <int MO, int R, int NW>
+struct wx_geom {
+  static constexpr int N = MO + R - 1, P = N * N, NT = 64 * NW;
+  static constexpr int NPG = N == 6 ? 4 : 2, PPG = P / NPG, NOG = NW / NPG, OCT = 32 * NOG;
+  static constexpr int PS = N == 6 ? 12 : 8;  // V pitch per (channel, tile): PPG values + pad
+  // exchange pitch per (channel, tile) pair: NPG slots of PS, padded so that 8 consecutive pairs'
+  // 16-B accesses fall on disjoint banks
+  static constexpr int XS = N == 6 ? 52 : 20;
+  static constexpr int ECH = NT / (NOG * 64);  // accumulator elements per exchange round
+  static_assert((N == 4 || N == 6) && NOG >= 1 && NPG * NOG == NW, "4x4 or 6x6 patches, whole wave groups");
+};
+
+// position (i, j) of the N x N grid <-> (group, slot): 6x6 -- quadrants (i / 3, j / 3), slot
+// (i % 3) * 3 + j % 3; 4x4 -- row pairs i / 2, slot (i % 2) * 4 + j
+template <int N>
+__host__ __device__ constexpr int wx_group(int i, int j) { return N == 6 ? (i / 3) * 2 + j / 3 : i / 2; }
+template <int N>
+__host__ __device__ constexpr int wx_slot(int i, int j) { return N == 6 ? (i % 3) * 3 + j % 3 : (i % 2) * 4 + j; }
+
+// 6-point transform B^T x (points 0, +-1, +-2): outputs o0 .. o0 + 2 (o0 = 0 or 3)
+template <int O0>
+__device__ __forceinline__ void bt6_half(const float (&x)[6], float (&t)[3]) {
+  if constexpr (O0 == 0) {
+    t[0] = fmaf(4.0f, x[0], fmaf(-5.0f, x[2], x[4]));
+    t[1] = fmaf(-4.0f, x[1] + x[2], x[3] + x[4]);
+    t[2] = fmaf(4.0f, x[1] - x[2], x[4] - x[3]);
+  } else {
+    t[0] = fmaf(2.0f, x[3] - x[1], x[4] - x[2]);
+    t[1] = fmaf(-2.0f, x[3] - x[1], x[4] - x[2]);
+    t[2] = fmaf(4.0f, x[1], fmaf(-5.0f, x[3], x[5]));
+  }
+}
+__device__ __forceinline__ void bt6(const float (&x)[6], float (&t)[6]) {
+  const float s12 = x[1] + x[2], d12 = x[1] - x[2], a = x[4] - x[2], b = x[3] - x[1];
+  t[0] = fmaf(4.0f, x[0], fmaf(-5.0f, x[2], x[4]));
+  t[1] = fmaf(-4.0f, s12, x[3] + x[4]);
+  t[2] = fmaf(4.0f, d12, x[4] - x[3]);
+  t[3] = fmaf(2.0f, b, a);
+  t[4] = fmaf(-2.0f, b, a);
+  t[5] = fmaf(4.0f, x[1], fmaf(-5.0f, x[3], x[5]));
+}
+// A^T x: F(4,3) rows (6 -> 4), F(2,5) rows (6 -> 2), F(2,3) rows (4 -> 2)
+template <int MO, int N>
+__device__ __forceinline__ void at_row(const float *x, float *y) {
+  if constexpr (N == 6) {
+    const float s1 = x[1] + x[2], d1 = x[1] - x[2], s2 = x[3] + x[4], d2 = x[3] - x[4];
+    y[0] = x[0] + s1 + s2;
+    if constexpr (MO == 4) {
+      y[1] = fmaf(2.0f, d2, d1);
+      y[2] = fmaf(4.0f, s2, s1);
+      y[3] = fmaf(8.0f, d2, d1) + x[5];
+    } else {
+      y[1] = fmaf(2.0f, d2, d1) + x[5];
+    }
+  } else {
+    y[0] = x[0] + x[1] + x[2];
+    y[1] = x[1] - x[2] - x[3];
+  }
+}
+
+// logical block of hardware block bid: blocks b, b + 8, ... share an XCD under round-robin placement,
+// so each XCD gets a contiguous run of units (the same OC tiles' U slices in its L2)
+__device__ __forceinline__ uint32_t wx_lb(uint32_t bid, uint32_t G) {
+  const uint32_t xcd = bid & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int MO, int R, int SP, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
+  using G = wx_geom<MO, R, NW>;
+  constexpr int N = G::N, P = G::P, NPG = G::NPG, PPG = G::PPG, NOG = G::NOG, OCT = G::OCT, PS = G::PS;
+  constexpr int XNT = G::NT;
+  constexpr int SCAP = SP * XNT;                // strip floats per slot
+  constexpr int VSZ = NPG * XC * XTT * PS;      // floats of one V buffer
+  constexpr int NLU = N == 6 ? 3 : 2;           // U loads per lane and k step (9 floats: 4 + 4 + 1; 8: 4 + 4)
+  static_assert(SP >= 1 && SP + 2 * NLU <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *const vbase = smem + 2 * SCAP;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pg = wave % NPG, og = wave / NPG;
+  const int li = lane & 31, kh = lane >> 5;
+  const uint32_t unit = wx_lb(blockIdx.x, gridDim.x);
+  // OC tile slowest: an XCD's run of units shares few OC tiles' U slices
+  const uint32_t oct = fdiv(unit, p.ngr_m, p.ngr_s);
+  const uint32_t oc0 = oct * OCT, g0 = (unit - oct * p.ngr) * XTT;
+  const uint32_t ipt = p.ipt;
+
+  auto tpos = [&](uint32_t tg, uint32_t &v, uint32_t &x) {  // virtual row, strip column of tile tg's patch
+    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    v = img * p.VH + MO * ty;
+    x = MO * tx;
+  };
+  uint32_t v0, x0u;
+  tpos(g0, v0, x0u);
+
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
+  const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
+
+  // ---- strip DMA plan (per lane, fixed for the unit): element f = j * NT + tid of the
+  // [4][RIN][WPM] image; the stage's first channel enters as the scalar soffset
+  uint32_t svo[SP];
+#pragma unroll
+  for (int j = 0; j < SP; ++j) {
+    const uint32_t f = (uint32_t)(j * XNT + tid);
+    const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
+    const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
+    const uint32_t v = v0 + s;
+    const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
+    const uint32_t iy = v - img * p.VH - p.pad;  // wraps (misses) in the top padding
+    const uint32_t ix = col - p.pad;             // wraps (misses) in the left padding
+    const bool ok = (c < (uint32_t)XC) & (ix < p.W) & (iy < p.H) & (img < p.B);
+    svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + ix) * 4u);
+  }
+  auto issue_strip = [&](int slot, uint32_t it) {  // stage it's strip (dead past the unit: no memory touched)
+    const bool live = it < ipt;
+    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u;
+#pragma unroll
+    for (int j = 0; j < SP; ++j) dma4s(live ? rsi : rnull, smem + slot * SCAP + j * XNT + tid, svo[j], ss);
+  };
+
+  // ---- U of stage it into registers: lane (li, kh) holds (input channel 4 it + 2 s + kh, output
+  // channel oc0 + 32 og + li), this wave's PPG positions
+  const uint32_t ocl = oc0 + (uint32_t)(32 * og + li);
+  uint32_t uoff[2][NLU];
+  {
+    const uint32_t rot = (ocl >> 2) & 3u;  // 4x4 bank: chunk x (row i) at ((x + rot) & 3) * 4
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t row = (uint32_t)(2 * s + kh) * p.OC32 + ocl;
+      if constexpr (N == 6) {
+        const uint32_t b = (row * 36u + (uint32_t)(PPG * pg)) * 4u;
+        uoff[s][0] = oob_unless(ocl < p.OC32, b);
+        uoff[s][1] = oob_unless(ocl < p.OC32, b + 16u);
+        uoff[s][2] = oob_unless(ocl < p.OC32, b + 32u);
+      } else {
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+          uoff[s][x] = oob_unless(ocl < p.OC32, (row * 16u + ((2u * pg + x + rot) & 3u) * 4u) * 4u);
+      }
+    }
+  }
+  float ur[2][PPG];
+  auto load_u = [&](int s, uint32_t it) {
+    const uint32_t su = it < ipt ? it * (uint32_t)XC * p.OC32 * (uint32_t)(P * 4) : 0x7fffff00u;  // dead: misses
+    const f32x4v a = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][0], su, 0));
+    const f32x4v b = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][1], su, 0));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ur[s][e] = a[e];
+      ur[s][4 + e] = b[e];
+    }
+    if constexpr (N == 6) ur[s][8] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsu, uoff[s][2], su, 0));
+  };
+
+  // ---- V fragments of k step s from buffer vb: (channel 2 s + kh, tile li), this group's slots
+  float vf[2][PPG];
+  auto load_vf = [&](int vb, int s) {
+    const float *const src = vbase + vb * VSZ + ((pg * XC + 2 * s + kh) * XTT + li) * PS;
+    const f32x4v a = *(const f32x4v *)src, b = *(const f32x4v *)(src + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      vf[s][e] = a[e];
+      vf[s][4 + e] = b[e];
+    }
+    if constexpr (N == 6) vf[s][8] = src[8];
+  };
+
+  // ---- input transform (threads 0..255: patch tid % 128 = (channel, tile), half tid / 128)
+  const uint32_t xpatch = (uint32_t)tid & 127u, xh = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 7);
+  const uint32_t xc = xpatch / XTT, xtt = xpatch % XTT;
+  uint32_t xoff = 0;  // float offset of the patch in a strip slot
+  {
+    const uint32_t tg = g0 + xtt;
+    if (tg < p.T) {
+      uint32_t v, x;
+      tpos(tg, v, x);
+      xoff = xc * p.RW + (v - v0) * p.WPM + x;
+    }
+  }
+  auto transform = [&](int slot, int vb) {
+    if (tid >= 256) return;  // NW = 8: waves 4..7 (uniform) make no patches
+    const float *const s = smem + slot * SCAP + xoff;
+    const uint32_t wpm = p.WPM;
+    float *const vd = vbase + vb * VSZ + (xc * XTT + xtt) * PS;
+    if constexpr (N == 6) {
+      // E = d B, this half's three columns c = 3 xh + c' (E[r][c] = (B^T d_r)[c]); V[i][c] = (B^T E[:, c])[i]
+      float e[6][3];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        float d[6];
+        if constexpr (MO == 4) {  // patch starts at a multiple of 4 floats
+          const f32x4v a = *(const f32x4v *)(s + r * wpm);
+          const f32x2v b = *(const f32x2v *)(s + r * wpm + 4);
+          d[0] = a[0]; d[1] = a[1]; d[2] = a[2]; d[3] = a[3]; d[4] = b[0]; d[5] = b[1];
+        } else {  // multiple of 2
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const f32x2v a = *(const f32x2v *)(s + r * wpm + 2 * q);
+            d[2 * q] = a[0];
+            d[2 * q + 1] = a[1];
+          }
+        }
+        if (xh) bt6_half<3>(d, e[r]);
+        else bt6_half<0>(d, e[r]);
+      }
+      float vcol[3][6];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float col[6] = {e[0][c], e[1][c], e[2][c], e[3][c], e[4][c], e[5][c]};
+        bt6(col, vcol[c]);
+      }
+      // groups (gi, xh), gi = 0, 1: slot (i % 3) * 3 + c
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        float *const dst = vd + (size_t)(2 * gi) * XC * XTT * PS + xh * XC * XTT * PS;
+        float w[9];
+#pragma unroll
+        for (int il = 0; il < 3; ++il)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) w[il * 3 + c] = vcol[c][3 * gi + il];
+        *(f32x4v *)dst = f32x4v{w[0], w[1], w[2], w[3]};
+        *(f32x4v *)(dst + 4) = f32x4v{w[4], w[5], w[6], w[7]};
+        dst[8] = w[8];
+      }
+    } else {
+      // F(2x2, 3x3): E = d B for all four rows, then V rows 2 xh, 2 xh + 1 (group xh)
+      float e[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x2v a = *(const f32x2v *)(s + r * wpm), b = *(const f32x2v *)(s + r * wpm + 2);
+        e[r][0] = a[0] - b[0];
+        e[r][1] = a[1] + b[0];
+        e[r][2] = b[0] - a[1];
+        e[r][3] = a[1] - b[1];
+      }
+      float w[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (xh) {
+          w[c] = e[2][c] - e[1][c];
+          w[4 + c] = e[1][c] - e[3][c];
+        } else {
+          w[c] = e[0][c] - e[2][c];
+          w[4 + c] = e[1][c] + e[2][c];
+        }
+      }
+      float *const dst = vd + xh * XC * XTT * PS;
+      *(f32x4v *)dst = f32x4v{w[0], w[1], w[2], w[3]};
+      *(f32x4v *)(dst + 4) = f32x4v{w[4], w[5], w[6], w[7]};
+    }
+  };
+
+  f32x16 acc[PPG];
+#pragma unroll
+  for (int q = 0; q < PPG; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
+
+  // ---- prologue: strips of stages 0 and 1, U(0); V(0)
+  issue_strip(0, 0);
+  issue_strip(1, 1);
+  load_u(0, 0);
+  load_u(1, 0);
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  transform(0, 0);
+
+  // per stage and lane, VMEM in issue order: strip(it + 2) (SP DMAs) right after the barrier, then
+  // U(it + 1) k step 0 (NLU loads) after the k-step-0 MFMAs, U(it + 1) k step 1 (NLU) at the end.
+  // Top of stage it: strip(it + 1) must have landed -> vmcnt(2 NLU); before k step 0's MFMAs U(it)
+  // step 0 -> vmcnt(NLU + SP); before k step 1's, U(it) step 1 -> vmcnt(SP + NLU)
+  for (uint32_t it = 0; it < ipt; ++it) {
+    const int vb = (int)(it & 1u);
+    vm_wait<2 * NLU>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // V(it) written, strip(it + 1) landed, strip(it)'s slot free
+    asm volatile("" ::: "memory");
+    issue_strip(vb, it + 2);
+    load_vf(vb, 0);
+    load_vf(vb, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    transform(vb ^ 1, vb ^ 1);  // strip(it + 1) -> V(it + 1)
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<NLU + SP>();
+#pragma unroll
+    for (int q = 0; q < PPG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_u(0, it + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<SP + NLU>();
+#pragma unroll
+    for (int q = 0; q < PPG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_u(1, it + 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the strips and V: the LDS is the exchange now
+  asm volatile("" ::: "memory");
+
+  // ---- epilogue: rounds of ECH accumulator elements; pair (og, e, lane) of the round meets its P
+  // values in thread pair = (og * ECH + e_local) * 64 + lane
+  constexpr int ECH = G::ECH, XS = G::XS;
+  float *const xb = smem;
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+  // the reader side of this thread: its pair's channel and tile (fixed over rounds except e)
+  const uint32_t rog = (uint32_t)tid / (ECH * 64), rel = ((uint32_t)tid / 64) % ECH, rlane = (uint32_t)tid & 63u;
+  const uint32_t rtile = g0 + (rlane & 31u);
+  const bool tvalid = rtile < p.T;
+  uint32_t obase = 0, oy0 = 0, ox0 = 0;
+  {
+    const uint32_t tg = tvalid ? rtile : 0u;
+    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    oy0 = MO * ty;
+    ox0 = MO * tx;
+    obase = img * p.OCOHW + oy0 * p.OW + ox0;
+  }
+#pragma unroll
+  for (int r0 = 0; r0 < 16; r0 += ECH) {
+    // write: this wave's PPG values of elements r0 .. r0 + ECH - 1
+#pragma unroll
+    for (int el = 0; el < ECH; ++el) {
+      float m[PPG];
+#pragma unroll
+      for (int q = 0; q < PPG; ++q) m[q] = acc[q][r0 + el];
+      float *const dst = xb + ((og * ECH + el) * 64 + lane) * XS + pg * PS;
+      *(f32x4v *)dst = f32x4v{m[0], m[1], m[2], m[3]};
+      *(f32x4v *)(dst + 4) = f32x4v{m[4], m[5], m[6], m[7]};
+      if constexpr (N == 6) dst[8] = m[8];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // read: the pair's N x N values, A^T M A, bias, residual, ReLU, store
+    {
+      float mm[N][N];
+      const float *const src = xb + (size_t)tid * XS;
+#pragma unroll
+      for (int g = 0; g < NPG; ++g) {
+        float m[PPG];
+        const f32x4v a = *(const f32x4v *)(src + g * PS), b = *(const f32x4v *)(src + g * PS + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          m[e] = a[e];
+          m[4 + e] = b[e];
+        }
+        if constexpr (N == 6) m[8] = src[g * PS + 8];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int j = 0; j < N; ++j)
+            if (wx_group<N>(i, j) == g) mm[i][j] = m[wx_slot<N>(i, j)];
+      }
+      float t[N][MO];  // T = M A (each row of M through A^T)
+#pragma unroll
+      for (int i = 0; i < N; ++i) at_row<MO, N>(mm[i], t[i]);
+      float y[MO][MO];  // Y = A^T T (each column of T)
+#pragma unroll
+      for (int x = 0; x < MO; ++x) {
+        float col[N], o[MO];
+#pragma unroll
+        for (int i = 0; i < N; ++i) col[i] = t[i][x];
+        at_row<MO, N>(col, o);
+#pragma unroll
+        for (int yy = 0; yy < MO; ++yy) y[yy][x] = o[yy];
+      }
+      const uint32_t e = (uint32_t)r0 + rel;
+      const uint32_t oc = oc0 + rog * 32u + 8u * (e >> 2) + 4u * (rlane >> 5) + (e & 3u);
+      const bool ok = tvalid & (oc < p.OC);
+      const float bb = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+      const uint32_t ob = obase + oc * p.OHW;
+#pragma unroll
+      for (int yy = 0; yy < MO; ++yy) {
+        if (p.vst) {  // uniform: OW % MO == 0 and MO-float aligned tensors -- a tile row is one store
+          typedef __attribute__((ext_vector_type(MO))) uint32_t uv_t;
+          const uint32_t off = oob_unless(ok & (oy0 + yy < p.OH), (ob + yy * p.OW) * 4u);
+          float z[MO];
+          uv_t rv = {};
+          if (p.res) {
+            if constexpr (MO == 4) rv = __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0);
+            else rv = __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0);
+          }
+          uv_t v;
+#pragma unroll
+          for (int x = 0; x < MO; ++x) {
+            z[x] = y[yy][x] + bb;
+            if (p.res) z[x] += __builtin_bit_cast(float, rv[x]);
+            z[x] = (p.relu && z[x] < 0.0f) ? 0.0f : z[x];
+            v[x] = __builtin_bit_cast(uint32_t, z[x]);
+          }
+          if constexpr (MO == 4) {
+            if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_SC1);
+            else __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_OUT);
+          } else {
+            if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_SC1);
+            else __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_OUT);
+          }
+          continue;
+        }
+#pragma unroll
+        for (int x = 0; x < MO; ++x) {
+          const bool in = ok & (oy0 + yy < p.OH) & (ox0 + x < p.OW);
+          const uint32_t off = oob_unless(in, (ob + yy * p.OW + x) * 4u);
+          float z = y[yy][x] + bb;
+          if (p.res) z += ld1(rsr, off);
+          z = (p.relu && z < 0.0f) ? 0.0f : z;
+          if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_SC1);
+          else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_OUT);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every reader done before the next round's writes
+    asm volatile("" ::: "memory");
+  }
+}
+
+template <int MO, int R, int SP, int NW>
+cfg_t wgx_cfg(const char *name) {
+  using G = wx_geom<MO, R, NW>;
+  cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW>;
+  c.dc = 5;
+  c.dc_ky = R;
+  c.dc_kx = R;
+  c.dc_s = MO;  // output tile
+  c.dc_rin = SP;
+  return c;
+}
+
+// Filter transform of the 6x6 forms: u[ic][oc][(group, slot)] = G g G^T (double, rounded once)
+template <int R>
+__global__ __launch_bounds__(256) void wx_pack_kernel(const float *__restrict__ w, float *__restrict__ u, uint32_t OC,
+                                                      uint32_t IC, uint32_t OC32, uint32_t IC4) {
+  const uint32_t e = blockIdx.x * 256u + threadIdx.x;  // ic * OC32 + oc
+  if (e >= IC4 * OC32) return;
+  const uint32_t ic = e / OC32, oc = e - ic * OC32;
+  const bool ok = oc < OC && ic < IC;
+  // G (6 x R) for points 0, 1, -1, 2, -2, infinity: row k = (q_k^0 .. q_k^{R-1}) / prod_{l != k} (q_k - q_l)
+  const double q[5] = {0.0, 1.0, -1.0, 2.0, -2.0};
+  double g[6][R];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    double den = 1.0;
+#pragma unroll
+    for (int l = 0; l < 5; ++l)
+      if (l != k) den *= q[k] - q[l];
+    double pw = 1.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      g[k][j] = pw / den;
+      pw *= q[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) g[5][j] = j == R - 1 ? 1.0 : 0.0;
+  double f[R][R];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int b = 0; b < R; ++b) f[a][b] = ok ? (double)w[((size_t)oc * IC + ic) * (R * R) + a * R + b] : 0.0;
+  double t[6][R];  // G f
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int b = 0; b < R; ++b) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) s += g[i][a] * f[a][b];
+      t[i][b] = s;
+    }
+  float *const dst = u + (size_t)e * 36;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < R; ++b) s += t[i][b] * g[j][b];
+      dst[wx_group<6>(i, j) * 9 + wx_slot<6>(i, j)] = (float)s;
+    }
+}
+
+}  // namespace
+
+std::vector<cfg_t> wgx_cfgs() {
+  // <MO, R, SP, NW>: output tile MO x MO, filter R x R (patch MO + R - 1), SP dword strip DMAs per
+  // lane and stage (the strip [4][RIN][WPM] must fit SP * 64 NW floats), NW waves per block
+  return {
+      wgx_cfg<4, 3, 4, 8>("wx43s4"),   wgx_cfg<4, 3, 8, 8>("wx43s8"),   wgx_cfg<4, 3, 12, 8>("wx43s12"),
+      wgx_cfg<2, 5, 3, 8>("wx25s3"),   wgx_cfg<2, 5, 6, 8>("wx25s6"),   wgx_cfg<2, 5, 10, 8>("wx25s10"),
+      wgx_cfg<2, 3, 3, 8>("wx23s3"),   wgx_cfg<2, 3, 6, 8>("wx23s6"),   wgx_cfg<2, 3, 10, 8>("wx23s10"),
+      // four waves (OC tile 32 / 64): twice the units, two blocks per CU -- the small-batch shapes
+      wgx_cfg<4, 3, 8, 4>("wx43s8w4"), wgx_cfg<4, 3, 16, 4>("wx43s16w4"),
+      wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
+      wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
+  };
+}
+
+size_t wx_bank_floats(uint32_t OC, uint32_t IC) { return (size_t)((IC + 3) & ~3u) * ((OC + 31) & ~31u) * 36; }
+
+int launch_wx_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, uint32_t R, bool first,
+                   bool last) {
+  uint32_t OC32 = (OC + 31) & ~31u, IC4 = (IC + 3) & ~3u;
+  const uint64_t n = (uint64_t)OC32 * IC4;
+  void *args[] = {(void *)&filts, (void *)&u, (void *)&OC, (void *)&IC, (void *)&OC32, (void *)&IC4};
+  const void *k = R == 3 ? (const void *)wx_pack_kernel<3> : (const void *)wx_pack_kernel<5>;
+  return bh::launch(ctx, k, dim3((uint32_t)((n + 255) / 256)), dim3(256), args, first, last, "wx_pack");
+}
+
+// Launch a position-split Winograd configuration: UNSUP unless a stride-1 R x R conv (R = the
+// configuration's) with pad <= R / 2, IC % 4 == 0, IC <= 512 for the 6x6 forms (their fp32
+// transform error), whose strips fit the configuration's slot. u: the bank of the configuration's
+// form (6x6: wx_pack; 4x4: bh_wino.hip's). One block per unit (whole units, no split).
+int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
+               float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
+               uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
+               bool first) {
+  (void)splits;
+  const uint32_t R = (uint32_t)c.dc_ky, MO = (uint32_t)c.dc_s, N = MO + R - 1;
+  if (KY != R || KX != R || sy != 1 || sx != 1 || py != px || py > R / 2)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for stride-1 square-padded convs of its kernel size");
+  if (IC % XC) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs IC % 4 == 0");
+  if (N == 6 && IC > 512) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " keeps IC <= 512 (fp32 transform error)");
+  const uint32_t pad = py;
+  const uint32_t OH = H + 2 * pad - R + 1, OW = W + 2 * pad - R + 1;
+  const uint32_t TH = (OH + MO - 1) / MO, TW = (OW + MO - 1) / MO, TPI = TH * TW;
+  const uint64_t T64 = (uint64_t)B * TPI;
+  const uint32_t VH = std::max(H + 2 * pad, MO * (TH - 1) + N);
+  const uint32_t WPM = (std::max(W + 2 * pad, MO * (TW - 1) + N) + 3) & ~3u;
+  if (T64 >= (1u << 30) || (uint64_t)B * VH >= (1u << 30)) return bh::fail(BH_UNSUP, "conv: too many Winograd tiles");
+  const uint32_t T = (uint32_t)T64, ngroups = (T + XTT - 1) / XTT;
+  auto vrow = [&](uint32_t tg) { return (tg / TPI) * VH + MO * ((tg % TPI) / TW); };
+  uint32_t rin = 0;
+  for (uint32_t gi = 0; gi < ngroups; ++gi) {
+    const uint32_t a = gi * XTT, b = std::min(T, a + XTT) - 1;
+    rin = std::max(rin, vrow(b) + N - vrow(a));
+  }
+  const uint32_t SP = (uint32_t)c.dc_rin, XNT = (uint32_t)c.NT;
+  if ((uint64_t)XC * rin * WPM > (uint64_t)SP * XNT)
+    return bh::fail(BH_UNSUP, std::string("conv: input strip too large for ") + c.name);
+  // (smaller strips than a configuration's slot are left to the configurations with fewer DMAs)
+  const uint64_t out_bytes = (uint64_t)B * out_ctot * OH * OW * 4;
+  if (out_bytes >= 0x7fffff00ull || (uint64_t)B * IC * H * W * 4 >= 0x7fffff00ull)
+    return bh::fail(BH_UNSUP, "conv: tensors too large for the Winograd kernel");
+  const uint32_t OC32 = (OC + 31) & ~31u, P = N * N;
+  const uint64_t ubytes = (uint64_t)((IC + 3) & ~3u) * OC32 * P * 4;
+  if (ubytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: Winograd bank too large");
+  WxArgs p{};
+  p.u = u; p.in = in; p.out = out; p.bias = bias; p.res = res;
+  p.u_bytes = (uint32_t)ubytes;
+  p.in_bytes = (uint32_t)((uint64_t)B * IC * H * W * 4);
+  p.out_bytes = (uint32_t)out_bytes;
+  p.OC = OC; p.OC32 = OC32; p.IC = IC; p.B = B; p.H = H; p.W = W; p.pad = pad;
+  p.OH = OH; p.OW = OW; p.OHW = OH * OW; p.HW = H * W; p.ICHW = IC * H * W; p.OCOHW = out_ctot * OH * OW;
+  p.TW = TW; p.TPI = TPI; p.VH = VH; p.T = T; p.WPM = WPM; p.RW = rin * WPM;
+  bh::fastdiv f = bh::make_fastdiv(TW); p.tw_m = f.m; p.tw_s = f.s;
+  f = bh::make_fastdiv(TPI); p.tpi_m = f.m; p.tpi_s = f.s;
+  f = bh::make_fastdiv(VH); p.vh_m = f.m; p.vh_s = f.s;
+  f = bh::make_fastdiv(WPM); p.wpm_m = f.m; p.wpm_s = f.s;
+  f = bh::make_fastdiv(p.RW); p.rw_m = f.m; p.rw_s = f.s;
+  p.ngr = ngroups;
+  f = bh::make_fastdiv(ngroups); p.ngr_m = f.m; p.ngr_s = f.s;
+  p.ipt = IC / XC;
+  p.relu = relu;
+  p.wt = wt;
+  p.vst = (OW % MO == 0 && ((uintptr_t)out % (4 * MO)) == 0 && ((uintptr_t)res % (4 * MO)) == 0) ? 1 : 0;
+  const uint32_t OCT = (uint32_t)c.BM, octiles = (OC + OCT - 1) / OCT;
+  const uint64_t units = (uint64_t)ngroups * octiles;
+  if (units >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many Winograd units");
+  // dynamic LDS: two strip slots + two V buffers, or the epilogue's exchange (512 pairs x pitch)
+  const uint32_t NPG = N == 6 ? 4 : 2, PS = N == 6 ? 12 : 8, XS = N == 6 ? 52 : 20;
+  const uint32_t lds = std::max(2 * SP * XNT + 2 * NPG * XC * XTT * PS, XNT * XS) * 4;
+  if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: LDS too small for ") + c.name);
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3((uint32_t)units, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
+}
+
+}  // namespace bhk

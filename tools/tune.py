@@ -41,7 +41,7 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
-    if name.startswith(("dc", "dm", "fcv", "ks", "wg")):
+    if name.startswith(("dc", "dm", "fcv", "ks", "wg", "wx")):
         return 1 << 30
     if name.startswith("gv"):
         m = re.search(r"w(\d+)", name)
@@ -167,6 +167,11 @@ def main():
                     if cn.startswith("wg"):  # Winograd 3x3: S = grid mode as stream-K; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 3 and s.sy == s.sx == 1 and s.py <= 1 and s.px <= 1:
                             cand += [(ci, 1), (ci, 5), (ci, 11), (ci, 15)]  # one block per CU (256 AGPRs)
+                        continue
+                    if cn.startswith("wx"):  # position-split Winograd: whole units; UNSUP for other ops
+                        r = 5 if cn.startswith("wx25") else 3
+                        if kind == 1 and s.KY == s.KX == r and s.sy == s.sx == 1 and s.py == s.px <= r // 2:
+                            cand.append((ci, 0))
                         continue
                     if cn.startswith("ks"):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 1 and s.sy == s.sx == 1 and s.py == s.px == 0:
