@@ -323,9 +323,11 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
   // blocks per OC tile: enough waves for every pixel unit, at most the CUs' share; a multiple of 8
+  // rounded DOWN where that still leaves a block per XCD: rounding up put G above the resident
+  // blocks (264 blocks at one block per CU: the last 8 started when the first ones ended, +50 %)
   uint64_t per = std::max<uint64_t>(1, ((uint64_t)ncu * bpc) / oct);
   per = std::min<uint64_t>(per, (npu + nw - 1) / nw);
-  per = (per + 7) / 8 * 8;
+  per = per >= 8 ? per / 8 * 8 : 8;
   const uint64_t G = per * oct;
   if (G >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: k1s grid too large");
   p.tiles_m = oct;

@@ -56,6 +56,9 @@ struct WxArgs {
   uint32_t ipt;               // stages per unit (IC / 4)
   int relu, wt;
   int vst;                    // OW % MO == 0 and out / res MO-float aligned: a tile row per store
+#ifdef BH_KTRACE
+  unsigned long long *trace;  // per-block device-clock marks (tools/ktrace.py)
+#endif
 };
 
 namespace {
@@ -131,7 +134,10 @@ __device__ __forceinline__ uint32_t wx_lb(uint32_t bid, uint32_t G) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int MO, int R, int SP, int NW>
+// DBG (diagnostic builds in the instrumented library only; wrong results by design): bit 0 = no input
+// transform in the stage loop, 1 = no MFMA, 2 = no strip DMA, 3 = no U loads, 4 = no V fragment
+// loads, 5 = no stage barrier
+template <int MO, int R, int SP, int NW, int DBG = 0>
 __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   using G = wx_geom<MO, R, NW>;
   constexpr int N = G::N, P = G::P, NPG = G::NPG, PPG = G::PPG, NOG = G::NOG, OCT = G::OCT, PS = G::PS;
@@ -146,6 +152,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pg = wave % NPG, og = wave / NPG;
+  KT(0);
   const int li = lane & 31, kh = lane >> 5;
   const uint32_t unit = wx_lb(blockIdx.x, gridDim.x);
   // OC tile slowest: an XCD's run of units shares few OC tiles' U slices
@@ -247,39 +254,57 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       xoff = xc * p.RW + (v - v0) * p.WPM + x;
     }
   }
-  auto transform = [&](int slot, int vb) {
-    if (tid >= 256) return;  // NW = 8: waves 4..7 (uniform) make no patches
-    const float *const s = smem + slot * SCAP + xoff;
-    const uint32_t wpm = p.WPM;
+  // in three phases, so that the patch reads land under MFMAs instead of in front of them: tx_read
+  // (h) reads patch rows 3h .. 3h + 2 (4x4: all four rows at h = 0), tx_e(h) makes their E = d B
+  // values, tx_v makes V = B^T E from the whole E and writes it (threads 0..255 only: NW = 8 leaves
+  // waves 4..7 without patches; the callers test xf, which is wave-uniform)
+  const bool xf = tid < 256;
+  constexpr int NRD = N == 6 ? 3 : 4, NCE = N == 6 ? 3 : 4;
+  float dr[NRD][N];
+  float e[N][NCE];
+  auto tx_read = [&](int slot, int h) {
+    const float *const s = smem + slot * SCAP + xoff + (uint32_t)(h * NRD) * p.WPM;
+#pragma unroll
+    for (int r = 0; r < NRD; ++r) {
+      if constexpr (N == 6 && MO == 4) {  // patch starts at a multiple of 4 floats
+        const f32x4v a = *(const f32x4v *)(s + r * p.WPM);
+        const f32x2v b = *(const f32x2v *)(s + r * p.WPM + 4);
+        dr[r][0] = a[0]; dr[r][1] = a[1]; dr[r][2] = a[2]; dr[r][3] = a[3]; dr[r][4] = b[0]; dr[r][5] = b[1];
+      } else {  // multiple of 2
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+          const f32x2v a = *(const f32x2v *)(s + r * p.WPM + 2 * q);
+          dr[r][2 * q] = a[0];
+          dr[r][2 * q + 1] = a[1];
+        }
+      }
+    }
+  };
+  auto tx_e = [&](int h) {
+#pragma unroll
+    for (int r = 0; r < NRD; ++r) {
+      if constexpr (N == 6) {
+        if (xh) bt6_half<3>(dr[r], e[h * NRD + r]);
+        else bt6_half<0>(dr[r], e[h * NRD + r]);
+      } else {  // E[r] = B^T d_r: (d0 - d2, d1 + d2, d2 - d1, d1 - d3)
+        e[r][0] = dr[r][0] - dr[r][2];
+        e[r][1] = dr[r][1] + dr[r][2];
+        e[r][2] = dr[r][2] - dr[r][1];
+        e[r][3] = dr[r][1] - dr[r][3];
+      }
+    }
+  };
+  auto tx_v = [&](int vb) {
     float *const vd = vbase + vb * VSZ + (xc * XTT + xtt) * PS;
     if constexpr (N == 6) {
-      // E = d B, this half's three columns c = 3 xh + c' (E[r][c] = (B^T d_r)[c]); V[i][c] = (B^T E[:, c])[i]
-      float e[6][3];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        float d[6];
-        if constexpr (MO == 4) {  // patch starts at a multiple of 4 floats
-          const f32x4v a = *(const f32x4v *)(s + r * wpm);
-          const f32x2v b = *(const f32x2v *)(s + r * wpm + 4);
-          d[0] = a[0]; d[1] = a[1]; d[2] = a[2]; d[3] = a[3]; d[4] = b[0]; d[5] = b[1];
-        } else {  // multiple of 2
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const f32x2v a = *(const f32x2v *)(s + r * wpm + 2 * q);
-            d[2 * q] = a[0];
-            d[2 * q + 1] = a[1];
-          }
-        }
-        if (xh) bt6_half<3>(d, e[r]);
-        else bt6_half<0>(d, e[r]);
-      }
+      // this half's three columns c = 3 xh + c' of E; V[i][c] = (B^T E[:, c])[i]; groups (gi, xh),
+      // slot (i % 3) * 3 + c'
       float vcol[3][6];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const float col[6] = {e[0][c], e[1][c], e[2][c], e[3][c], e[4][c], e[5][c]};
         bt6(col, vcol[c]);
       }
-      // groups (gi, xh), gi = 0, 1: slot (i % 3) * 3 + c
 #pragma unroll
       for (int gi = 0; gi < 2; ++gi) {
         float *const dst = vd + (size_t)(2 * gi) * XC * XTT * PS + xh * XC * XTT * PS;
@@ -293,16 +318,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
         dst[8] = w[8];
       }
     } else {
-      // F(2x2, 3x3): E = d B for all four rows, then V rows 2 xh, 2 xh + 1 (group xh)
-      float e[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const f32x2v a = *(const f32x2v *)(s + r * wpm), b = *(const f32x2v *)(s + r * wpm + 2);
-        e[r][0] = a[0] - b[0];
-        e[r][1] = a[1] + b[0];
-        e[r][2] = b[0] - a[1];
-        e[r][3] = a[1] - b[1];
-      }
+      // F(2x2, 3x3): V rows 2 xh, 2 xh + 1 (group xh)
       float w[8];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -319,6 +335,16 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       *(f32x4v *)(dst + 4) = f32x4v{w[4], w[5], w[6], w[7]};
     }
   };
+  auto transform = [&](int slot, int vb) {  // all phases at once (the prologue)
+    if (!xf) return;
+    tx_read(slot, 0);
+    tx_e(0);
+    if constexpr (N == 6) {
+      tx_read(slot, 1);
+      tx_e(1);
+    }
+    tx_v(vb);
+  };
 
   f32x16 acc[PPG];
 #pragma unroll
@@ -326,15 +352,17 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
 
-  // ---- prologue: strips of stages 0 and 1, U(0); V(0)
+  // ---- prologue: strips of stages 0 and 1, then U(0) (still in flight while V(0) is made: the
+  // loop's first waits count on exactly the steady state's [strip][U k0][U k1] order)
   issue_strip(0, 0);
   issue_strip(1, 1);
   load_u(0, 0);
   load_u(1, 0);
-  vm_wait<0>();
+  vm_wait<2 * NLU>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   transform(0, 0);
+  KT(1);
 
   // per stage and lane, VMEM in issue order: strip(it + 2) (SP DMAs) right after the barrier, then
   // U(it + 1) k step 0 (NLU loads) after the k-step-0 MFMAs, U(it + 1) k step 1 (NLU) at the end.
@@ -344,31 +372,52 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     const int vb = (int)(it & 1u);
     vm_wait<2 * NLU>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // V(it) written, strip(it + 1) landed, strip(it)'s slot free
+    if constexpr ((DBG & 32) == 0) __builtin_amdgcn_s_barrier();  // V(it) written, strip(it + 1) landed, strip(it)'s slot free
     asm volatile("" ::: "memory");
-    issue_strip(vb, it + 2);
-    load_vf(vb, 0);
-    load_vf(vb, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    transform(vb ^ 1, vb ^ 1);  // strip(it + 1) -> V(it + 1)
+    if constexpr ((DBG & 4) == 0) issue_strip(vb, it + 2);
+    else if constexpr ((DBG & 64) == 0) issue_strip(vb, ipt);  // dead: the same VMEM count, no memory touched
+    if constexpr ((DBG & 16) == 0) {
+      load_vf(vb, 0);
+      load_vf(vb, 1);
+    }
+    // strip(it + 1) -> V(it + 1) in three phases around the MFMA groups (its reads land under them)
+    constexpr bool XF = (DBG & 1) == 0;
+    if (XF && xf) tx_read(vb ^ 1, 0);
     __builtin_amdgcn_sched_barrier(0);
     vm_wait<NLU + SP>();
 #pragma unroll
-    for (int q = 0; q < PPG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+    for (int q = 0; q < PPG; ++q) {
+      if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+      else asm volatile("" ::"v"(ur[0][q]), "v"(vf[0][q]));
+    }
     __builtin_amdgcn_sched_barrier(0);
-    load_u(0, it + 1);
+    if constexpr ((DBG & 8) == 0) load_u(0, it + 1);
+    else if constexpr ((DBG & 128) == 0) load_u(0, ipt);  // dead loads (misses): the same VMEM count
+    if (XF && xf) {
+      tx_e(0);
+      if constexpr (N == 6) tx_read(vb ^ 1, 1);
+    }
     __builtin_amdgcn_sched_barrier(0);
     vm_wait<SP + NLU>();
 #pragma unroll
-    for (int q = 0; q < PPG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+    for (int q = 0; q < PPG; ++q) {
+      if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+      else asm volatile("" ::"v"(ur[1][q]), "v"(vf[1][q]));
+    }
     __builtin_amdgcn_sched_barrier(0);
-    load_u(1, it + 1);
+    if constexpr ((DBG & 8) == 0) load_u(1, it + 1);
+    else if constexpr ((DBG & 128) == 0) load_u(1, ipt);
+    if (XF && xf) {
+      if constexpr (N == 6) tx_e(1);
+      tx_v(vb ^ 1);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   vm_wait<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // every wave done with the strips and V: the LDS is the exchange now
   asm volatile("" ::: "memory");
+  KT(2);
 
   // ---- epilogue: rounds of ECH accumulator elements; pair (og, e, lane) of the round meets its P
   // values in thread pair = (og * ECH + e_local) * 64 + lane
@@ -381,6 +430,16 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   const uint32_t rog = (uint32_t)tid / (ECH * 64), rel = ((uint32_t)tid / 64) % ECH, rlane = (uint32_t)tid & 63u;
   const uint32_t rtile = g0 + (rlane & 31u);
   const bool tvalid = rtile < p.T;
+  // this thread's bias values of every round, loaded before the first round (one memory latency,
+  // not one per round)
+  constexpr int NR = 16 / ECH;
+  float rbias[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const uint32_t e = (uint32_t)(r * ECH) + rel;
+    const uint32_t oc = oc0 + rog * 32u + 8u * (e >> 2) + 4u * (rlane >> 5) + (e & 3u);
+    rbias[r] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+  }
   uint32_t obase = 0, oy0 = 0, ox0 = 0;
   {
     const uint32_t tg = tvalid ? rtile : 0u;
@@ -442,7 +501,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       const uint32_t e = (uint32_t)r0 + rel;
       const uint32_t oc = oc0 + rog * 32u + 8u * (e >> 2) + 4u * (rlane >> 5) + (e & 3u);
       const bool ok = tvalid & (oc < p.OC);
-      const float bb = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+      const float bb = rbias[r0 / ECH];
       const uint32_t ob = obase + oc * p.OHW;
 #pragma unroll
       for (int yy = 0; yy < MO; ++yy) {
@@ -450,19 +509,23 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
           typedef __attribute__((ext_vector_type(MO))) uint32_t uv_t;
           const uint32_t off = oob_unless(ok & (oy0 + yy < p.OH), (ob + yy * p.OW) * 4u);
           float z[MO];
-          uv_t rv = {};
+          // (whole-vector bit casts only: hipcc miscompiles a bit cast of one vector component,
+          // DESIGN.md §3.11)
+          typedef __attribute__((ext_vector_type(MO))) float fv_t;
+          fv_t rv = {};
           if (p.res) {
-            if constexpr (MO == 4) rv = __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0);
-            else rv = __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0);
+            if constexpr (MO == 4) rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0));
+            else rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0));
           }
-          uv_t v;
+          fv_t zv;
 #pragma unroll
           for (int x = 0; x < MO; ++x) {
             z[x] = y[yy][x] + bb;
-            if (p.res) z[x] += __builtin_bit_cast(float, rv[x]);
+            if (p.res) z[x] += rv[x];
             z[x] = (p.relu && z[x] < 0.0f) ? 0.0f : z[x];
-            v[x] = __builtin_bit_cast(uint32_t, z[x]);
+            zv[x] = z[x];
           }
+          const uv_t v = __builtin_bit_cast(uv_t, zv);
           if constexpr (MO == 4) {
             if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_SC1);
             else __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_OUT);
@@ -488,13 +551,15 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     __builtin_amdgcn_s_barrier();  // every reader done before the next round's writes
     asm volatile("" ::: "memory");
   }
+  vm_wait<0>();
+  KT(4);
 }
 
-template <int MO, int R, int SP, int NW>
+template <int MO, int R, int SP, int NW, int DBG = 0>
 cfg_t wgx_cfg(const char *name) {
   using G = wx_geom<MO, R, NW>;
   cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW>;
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, DBG>;
   c.dc = 5;
   c.dc_ky = R;
   c.dc_kx = R;
@@ -569,6 +634,18 @@ std::vector<cfg_t> wgx_cfgs() {
       wgx_cfg<4, 3, 8, 4>("wx43s8w4"), wgx_cfg<4, 3, 16, 4>("wx43s16w4"),
       wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
       wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
+#ifdef BH_KTRACE
+      // diagnostic builds of wx43s12 / wx25s6 (wrong results by design): one part of the stage dropped
+      wgx_cfg<4, 3, 12, 8, 1>("xwx43_noxf"), wgx_cfg<4, 3, 12, 8, 2>("xwx43_nomfma"),
+      wgx_cfg<4, 3, 12, 8, 4>("xwx43_nodma"), wgx_cfg<4, 3, 12, 8, 8>("xwx43_nou"),
+      wgx_cfg<4, 3, 12, 8, 16>("xwx43_novf"), wgx_cfg<4, 3, 12, 8, 32>("xwx43_nobar"),
+      wgx_cfg<4, 3, 12, 8, 29>("xwx43_onlymfma"), wgx_cfg<4, 3, 12, 8, 30>("xwx43_onlyxf"),
+      // 6 bit: no strip DMA instructions at all, 7 bit: no U load instructions at all
+      wgx_cfg<4, 3, 12, 8, 29 + 64 + 128>("xwx43_puremfma"), wgx_cfg<4, 3, 12, 8, 29 + 64 + 128 + 32>("xwx43_puremfma_nobar"),
+      wgx_cfg<4, 3, 12, 8, 4 + 64>("xwx43_nodmaissue"),
+      wgx_cfg<2, 5, 6, 8, 1>("xwx25_noxf"), wgx_cfg<2, 5, 6, 8, 2>("xwx25_nomfma"),
+      wgx_cfg<2, 5, 6, 8, 8>("xwx25_nou"), wgx_cfg<2, 5, 6, 8, 29>("xwx25_onlymfma"),
+#endif
   };
 }
 
@@ -650,6 +727,9 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
   void *args[] = {&p};
   return bh::launch(ctx, k, dim3((uint32_t)units, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
 }

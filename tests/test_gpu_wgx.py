@@ -132,7 +132,7 @@ def test_wx_residual_and_slab(dev, cn):
         dev.tune_set(1, -1, 0)
 
 
-@pytest.mark.parametrize("cn", [n for n in WX if n in ("wx43s8", "wx25s6w4", "wx23s6")])
+@pytest.mark.parametrize("cn", [n for n in WX if n in ("wx43s8", "wx25s12w4", "wx23s6")])
 def test_wx_dword_aligned_pointers(dev, cn):
     """Input and output pointers one float past a 16-B boundary (a caller's sub-buffer): the strip
     DMA takes any dword alignment, and the tile-row vector stores fall back to dword stores."""
