@@ -53,7 +53,10 @@ struct WxArgs {
   uint32_t WPM, RW;           // strip pitch, RIN * WPM
   uint32_t tw_m, tw_s, tpi_m, tpi_s, vh_m, vh_s, wpm_m, wpm_s, rw_m, rw_s;
   uint32_t ngr, ngr_m, ngr_s; // tile groups (+ fastdiv)
-  uint32_t ipt;               // stages per unit (IC / 4)
+  uint32_t ipt, ipt_m, ipt_s; // stages per unit (IC / 4) (+ fastdiv)
+  uint32_t ipb, total_it;     // stream-K: iterations per block, in all
+  float *ws;                  // stream-K slabs, two per block
+  uint32_t *cnt;              // arrival tickets, one per unit
   int relu, wt;
   int vst;                    // OW % MO == 0 and out / res MO-float aligned: a tile row per store
 #ifdef BH_KTRACE
@@ -137,7 +140,10 @@ __device__ __forceinline__ uint32_t wx_lb(uint32_t bid, uint32_t G) {
 // DBG (diagnostic builds in the instrumented library only; wrong results by design): bit 0 = no input
 // transform in the stage loop, 1 = no MFMA, 2 = no strip DMA, 3 = no U loads, 4 = no V fragment
 // loads, 5 = no stage barrier
-template <int MO, int R, int SP, int NW, int DBG = 0>
+// SK = 0: one block per unit (whole units); SK = 1: a persistent stream-K grid dealing the (unit, stage)
+// iterations equally between the blocks; a unit cut between blocks is summed after the output
+// transform (linear) by its last-arriving block in block order (bitwise reproducible)
+template <int MO, int R, int SP, int NW, int SK, int DBG = 0>
 __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   using G = wx_geom<MO, R, NW>;
   constexpr int N = G::N, P = G::P, NPG = G::NPG, PPG = G::PPG, NOG = G::NOG, OCT = G::OCT, PS = G::PS;
@@ -145,6 +151,8 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   constexpr int SCAP = SP * XNT;                // strip floats per slot
   constexpr int VSZ = NPG * XC * XTT * PS;      // floats of one V buffer
   constexpr int NLU = N == 6 ? 3 : 2;           // U loads per lane and k step (9 floats: 4 + 4 + 1; 8: 4 + 4)
+  constexpr int ECH = G::ECH, XS = G::XS, NR = 16 / ECH, MM = MO * MO;
+  constexpr int FLAG = (2 * SCAP + 2 * VSZ > XNT * XS ? 2 * SCAP + 2 * VSZ : XNT * XS);  // LDS word: last arriver
   static_assert(SP >= 1 && SP + 2 * NLU <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *const vbase = smem + 2 * SCAP;
@@ -154,11 +162,12 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   const int pg = wave % NPG, og = wave / NPG;
   KT(0);
   const int li = lane & 31, kh = lane >> 5;
-  const uint32_t unit = wx_lb(blockIdx.x, gridDim.x);
-  // OC tile slowest: an XCD's run of units shares few OC tiles' U slices
-  const uint32_t oct = fdiv(unit, p.ngr_m, p.ngr_s);
-  const uint32_t oc0 = oct * OCT, g0 = (unit - oct * p.ngr) * XTT;
+  const uint32_t lb = wx_lb(blockIdx.x, gridDim.x);
   const uint32_t ipt = p.ipt;
+  // this block's iterations: SK -- [lb * ipb, + ipb); else unit lb. OC tile slowest in the unit order:
+  // an XCD's run of units shares few OC tiles' U slices
+  const uint32_t it0 = SK ? lb * p.ipb : lb * ipt;
+  const uint32_t it1 = SK ? min(p.total_it, it0 + p.ipb) : it0 + ipt;
 
   auto tpos = [&](uint32_t tg, uint32_t &v, uint32_t &x) {  // virtual row, strip column of tile tg's patch
     const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
@@ -166,40 +175,40 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     v = img * p.VH + MO * ty;
     x = MO * tx;
   };
-  uint32_t v0, x0u;
-  tpos(g0, v0, x0u);
 
   const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
   const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
   const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
 
-  // ---- strip DMA plan (per lane, fixed for the unit): element f = j * NT + tid of the
-  // [4][RIN][WPM] image; the stage's first channel enters as the scalar soffset
+  // ---- per-unit state (setup_unit): the unit's OC tile and tile group, the strip DMA plan (per
+  // lane: element f = j * NT + tid of the [4][RIN][WPM] image; the stage's first channel enters as
+  // the scalar soffset), the U offsets, the patch offset; sb = the end of the stages run now
+  uint32_t oc0 = 0, g0 = 0, sb = 0, xoff = 0;
   uint32_t svo[SP];
-#pragma unroll
-  for (int j = 0; j < SP; ++j) {
-    const uint32_t f = (uint32_t)(j * XNT + tid);
-    const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
-    const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
-    const uint32_t v = v0 + s;
-    const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
-    const uint32_t iy = v - img * p.VH - p.pad;  // wraps (misses) in the top padding
-    const uint32_t ix = col - p.pad;             // wraps (misses) in the left padding
-    const bool ok = (c < (uint32_t)XC) & (ix < p.W) & (iy < p.H) & (img < p.B);
-    svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + ix) * 4u);
-  }
-  auto issue_strip = [&](int slot, uint32_t it) {  // stage it's strip (dead past the unit: no memory touched)
-    const bool live = it < ipt;
-    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u;
-#pragma unroll
-    for (int j = 0; j < SP; ++j) dma4s(live ? rsi : rnull, smem + slot * SCAP + j * XNT + tid, svo[j], ss);
-  };
-
-  // ---- U of stage it into registers: lane (li, kh) holds (input channel 4 it + 2 s + kh, output
-  // channel oc0 + 32 og + li), this wave's PPG positions
-  const uint32_t ocl = oc0 + (uint32_t)(32 * og + li);
   uint32_t uoff[2][NLU];
-  {
+  const uint32_t xpatch = (uint32_t)tid & 127u, xh = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 7);
+  const uint32_t xc = xpatch / XTT, xtt = xpatch % XTT;
+  auto setup_unit = [&](uint32_t t) {
+    const uint32_t oct = fdiv(t, p.ngr_m, p.ngr_s);
+    oc0 = oct * OCT;
+    g0 = (t - oct * p.ngr) * XTT;
+    uint32_t v0, x0u;
+    tpos(g0, v0, x0u);
+#pragma unroll
+    for (int j = 0; j < SP; ++j) {
+      const uint32_t f = (uint32_t)(j * XNT + tid);
+      const uint32_t c = fdiv(f, p.rw_m, p.rw_s), rr = f - c * p.RW;
+      const uint32_t s = fdiv(rr, p.wpm_m, p.wpm_s), col = rr - s * p.WPM;
+      const uint32_t v = v0 + s;
+      const uint32_t img = fdiv(v, p.vh_m, p.vh_s);
+      const uint32_t iy = v - img * p.VH - p.pad;  // wraps (misses) in the top padding
+      const uint32_t ix = col - p.pad;             // wraps (misses) in the left padding
+      const bool ok = (c < (uint32_t)XC) & (ix < p.W) & (iy < p.H) & (img < p.B);
+      svo[j] = oob_unless(ok, (img * p.ICHW + c * p.HW + iy * p.W + ix) * 4u);
+    }
+    // U of stage it: lane (li, kh) holds (input channel 4 it + 2 s + kh, output channel oc0 + 32 og +
+    // li), this wave's PPG positions
+    const uint32_t ocl = oc0 + (uint32_t)(32 * og + li);
     const uint32_t rot = (ocl >> 2) & 3u;  // 4x4 bank: chunk x (row i) at ((x + rot) & 3) * 4
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -215,10 +224,23 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
           uoff[s][x] = oob_unless(ocl < p.OC32, (row * 16u + ((2u * pg + x + rot) & 3u) * 4u) * 4u);
       }
     }
-  }
+    xoff = 0;  // float offset of this thread's patch in a strip slot
+    const uint32_t tg = g0 + xtt;
+    if (tg < p.T) {
+      uint32_t v, x;
+      tpos(tg, v, x);
+      xoff = xc * p.RW + (v - v0) * p.WPM + x;
+    }
+  };
+  auto issue_strip = [&](int slot, uint32_t it) {  // stage it's strip (dead past the run: no memory touched)
+    const bool live = it < sb;
+    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u;
+#pragma unroll
+    for (int j = 0; j < SP; ++j) dma4s(live ? rsi : rnull, smem + slot * SCAP + j * XNT + tid, svo[j], ss);
+  };
   float ur[2][PPG];
   auto load_u = [&](int s, uint32_t it) {
-    const uint32_t su = it < ipt ? it * (uint32_t)XC * p.OC32 * (uint32_t)(P * 4) : 0x7fffff00u;  // dead: misses
+    const uint32_t su = it < sb ? it * (uint32_t)XC * p.OC32 * (uint32_t)(P * 4) : 0x7fffff00u;  // dead: misses
     const f32x4v a = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][0], su, 0));
     const f32x4v b = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][1], su, 0));
 #pragma unroll
@@ -242,22 +264,11 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     if constexpr (N == 6) vf[s][8] = src[8];
   };
 
-  // ---- input transform (threads 0..255: patch tid % 128 = (channel, tile), half tid / 128)
-  const uint32_t xpatch = (uint32_t)tid & 127u, xh = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 7);
-  const uint32_t xc = xpatch / XTT, xtt = xpatch % XTT;
-  uint32_t xoff = 0;  // float offset of the patch in a strip slot
-  {
-    const uint32_t tg = g0 + xtt;
-    if (tg < p.T) {
-      uint32_t v, x;
-      tpos(tg, v, x);
-      xoff = xc * p.RW + (v - v0) * p.WPM + x;
-    }
-  }
-  // in three phases, so that the patch reads land under MFMAs instead of in front of them: tx_read
-  // (h) reads patch rows 3h .. 3h + 2 (4x4: all four rows at h = 0), tx_e(h) makes their E = d B
-  // values, tx_v makes V = B^T E from the whole E and writes it (threads 0..255 only: NW = 8 leaves
-  // waves 4..7 without patches; the callers test xf, which is wave-uniform)
+  // ---- input transform (threads 0..255: patch tid % 128 = (channel, tile), half tid / 128), in
+  // three phases, so that the patch reads land under MFMAs instead of in front of them: tx_read(h)
+  // reads patch rows 3h .. 3h + 2 (4x4: all four rows at h = 0), tx_e(h) makes their E = d B values,
+  // tx_v makes V = B^T E from the whole E and writes it (NW = 8 leaves waves 4..7 without patches;
+  // the callers test xf, which is wave-uniform)
   const bool xf = tid < 256;
   constexpr int NRD = N == 6 ? 3 : 4, NCE = N == 6 ? 3 : 4;
   float dr[NRD][N];
@@ -346,220 +357,309 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     tx_v(vb);
   };
 
-  f32x16 acc[PPG];
-#pragma unroll
-  for (int q = 0; q < PPG; ++q)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
-
-  // ---- prologue: strips of stages 0 and 1, then U(0) (still in flight while V(0) is made: the
-  // loop's first waits count on exactly the steady state's [strip][U k0][U k1] order)
-  issue_strip(0, 0);
-  issue_strip(1, 1);
-  load_u(0, 0);
-  load_u(1, 0);
-  vm_wait<2 * NLU>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  transform(0, 0);
-  KT(1);
-
-  // per stage and lane, VMEM in issue order: strip(it + 2) (SP DMAs) right after the barrier, then
-  // U(it + 1) k step 0 (NLU loads) after the k-step-0 MFMAs, U(it + 1) k step 1 (NLU) at the end.
-  // Top of stage it: strip(it + 1) must have landed -> vmcnt(2 NLU); before k step 0's MFMAs U(it)
-  // step 0 -> vmcnt(NLU + SP); before k step 1's, U(it) step 1 -> vmcnt(SP + NLU)
-  for (uint32_t it = 0; it < ipt; ++it) {
-    const int vb = (int)(it & 1u);
-    vm_wait<2 * NLU>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr ((DBG & 32) == 0) __builtin_amdgcn_s_barrier();  // V(it) written, strip(it + 1) landed, strip(it)'s slot free
-    asm volatile("" ::: "memory");
-    if constexpr ((DBG & 4) == 0) issue_strip(vb, it + 2);
-    else if constexpr ((DBG & 64) == 0) issue_strip(vb, ipt);  // dead: the same VMEM count, no memory touched
-    if constexpr ((DBG & 16) == 0) {
-      load_vf(vb, 0);
-      load_vf(vb, 1);
-    }
-    // strip(it + 1) -> V(it + 1) in three phases around the MFMA groups (its reads land under them)
-    constexpr bool XF = (DBG & 1) == 0;
-    if (XF && xf) tx_read(vb ^ 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    vm_wait<NLU + SP>();
-#pragma unroll
-    for (int q = 0; q < PPG; ++q) {
-      if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
-      else asm volatile("" ::"v"(ur[0][q]), "v"(vf[0][q]));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((DBG & 8) == 0) load_u(0, it + 1);
-    else if constexpr ((DBG & 128) == 0) load_u(0, ipt);  // dead loads (misses): the same VMEM count
-    if (XF && xf) {
-      tx_e(0);
-      if constexpr (N == 6) tx_read(vb ^ 1, 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    vm_wait<SP + NLU>();
-#pragma unroll
-    for (int q = 0; q < PPG; ++q) {
-      if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
-      else asm volatile("" ::"v"(ur[1][q]), "v"(vf[1][q]));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((DBG & 8) == 0) load_u(1, it + 1);
-    else if constexpr ((DBG & 128) == 0) load_u(1, ipt);
-    if (XF && xf) {
-      if constexpr (N == 6) tx_e(1);
-      tx_v(vb ^ 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  vm_wait<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done with the strips and V: the LDS is the exchange now
-  asm volatile("" ::: "memory");
-  KT(2);
-
-  // ---- epilogue: rounds of ECH accumulator elements; pair (og, e, lane) of the round meets its P
-  // values in thread pair = (og * ECH + e_local) * 64 + lane
-  constexpr int ECH = G::ECH, XS = G::XS;
+  // ---- epilogue pieces: pair (og, e, lane) of an exchange round meets its P values in thread
+  // pair = (og * ECH + e_local) * 64 + lane; store_y adds bias, residual and ReLU and stores
   float *const xb = smem;
   const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
-  // the reader side of this thread: its pair's channel and tile (fixed over rounds except e)
   const uint32_t rog = (uint32_t)tid / (ECH * 64), rel = ((uint32_t)tid / 64) % ECH, rlane = (uint32_t)tid & 63u;
-  const uint32_t rtile = g0 + (rlane & 31u);
-  const bool tvalid = rtile < p.T;
-  // this thread's bias values of every round, loaded before the first round (one memory latency,
-  // not one per round)
-  constexpr int NR = 16 / ECH;
-  float rbias[NR];
+  auto store_y = [&](int r, const float (&y)[MO][MO], float bb, bool tvalid, uint32_t obase, uint32_t oy0,
+                     uint32_t ox0) {
+    const uint32_t ee = (uint32_t)(r * ECH) + rel;
+    const uint32_t oc = oc0 + rog * 32u + 8u * (ee >> 2) + 4u * (rlane >> 5) + (ee & 3u);
+    const bool ok = tvalid & (oc < p.OC);
+    const uint32_t ob = obase + oc * p.OHW;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const uint32_t e = (uint32_t)(r * ECH) + rel;
-    const uint32_t oc = oc0 + rog * 32u + 8u * (e >> 2) + 4u * (rlane >> 5) + (e & 3u);
-    rbias[r] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
-  }
-  uint32_t obase = 0, oy0 = 0, ox0 = 0;
-  {
-    const uint32_t tg = tvalid ? rtile : 0u;
-    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
-    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
-    oy0 = MO * ty;
-    ox0 = MO * tx;
-    obase = img * p.OCOHW + oy0 * p.OW + ox0;
-  }
-#pragma unroll
-  for (int r0 = 0; r0 < 16; r0 += ECH) {
-    // write: this wave's PPG values of elements r0 .. r0 + ECH - 1
-#pragma unroll
-    for (int el = 0; el < ECH; ++el) {
-      float m[PPG];
-#pragma unroll
-      for (int q = 0; q < PPG; ++q) m[q] = acc[q][r0 + el];
-      float *const dst = xb + ((og * ECH + el) * 64 + lane) * XS + pg * PS;
-      *(f32x4v *)dst = f32x4v{m[0], m[1], m[2], m[3]};
-      *(f32x4v *)(dst + 4) = f32x4v{m[4], m[5], m[6], m[7]};
-      if constexpr (N == 6) dst[8] = m[8];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // read: the pair's N x N values, A^T M A, bias, residual, ReLU, store
-    {
-      float mm[N][N];
-      const float *const src = xb + (size_t)tid * XS;
-#pragma unroll
-      for (int g = 0; g < NPG; ++g) {
-        float m[PPG];
-        const f32x4v a = *(const f32x4v *)(src + g * PS), b = *(const f32x4v *)(src + g * PS + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          m[e] = a[e];
-          m[4 + e] = b[e];
+    for (int yy = 0; yy < MO; ++yy) {
+      if (p.vst) {  // uniform: OW % MO == 0 and MO-float aligned tensors -- a tile row is one store
+        typedef __attribute__((ext_vector_type(MO))) uint32_t uv_t;
+        const uint32_t off = oob_unless(ok & (oy0 + yy < p.OH), (ob + yy * p.OW) * 4u);
+        float z[MO];
+        // (whole-vector bit casts only: hipcc miscompiles a bit cast of one vector component,
+        // DESIGN.md §3.11)
+        typedef __attribute__((ext_vector_type(MO))) float fv_t;
+        fv_t rv = {};
+        if (p.res) {
+          if constexpr (MO == 4) rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0));
+          else rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0));
         }
-        if constexpr (N == 6) m[8] = src[g * PS + 8];
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-          for (int j = 0; j < N; ++j)
-            if (wx_group<N>(i, j) == g) mm[i][j] = m[wx_slot<N>(i, j)];
-      }
-      float t[N][MO];  // T = M A (each row of M through A^T)
-#pragma unroll
-      for (int i = 0; i < N; ++i) at_row<MO, N>(mm[i], t[i]);
-      float y[MO][MO];  // Y = A^T T (each column of T)
-#pragma unroll
-      for (int x = 0; x < MO; ++x) {
-        float col[N], o[MO];
-#pragma unroll
-        for (int i = 0; i < N; ++i) col[i] = t[i][x];
-        at_row<MO, N>(col, o);
-#pragma unroll
-        for (int yy = 0; yy < MO; ++yy) y[yy][x] = o[yy];
-      }
-      const uint32_t e = (uint32_t)r0 + rel;
-      const uint32_t oc = oc0 + rog * 32u + 8u * (e >> 2) + 4u * (rlane >> 5) + (e & 3u);
-      const bool ok = tvalid & (oc < p.OC);
-      const float bb = rbias[r0 / ECH];
-      const uint32_t ob = obase + oc * p.OHW;
-#pragma unroll
-      for (int yy = 0; yy < MO; ++yy) {
-        if (p.vst) {  // uniform: OW % MO == 0 and MO-float aligned tensors -- a tile row is one store
-          typedef __attribute__((ext_vector_type(MO))) uint32_t uv_t;
-          const uint32_t off = oob_unless(ok & (oy0 + yy < p.OH), (ob + yy * p.OW) * 4u);
-          float z[MO];
-          // (whole-vector bit casts only: hipcc miscompiles a bit cast of one vector component,
-          // DESIGN.md §3.11)
-          typedef __attribute__((ext_vector_type(MO))) float fv_t;
-          fv_t rv = {};
-          if (p.res) {
-            if constexpr (MO == 4) rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0));
-            else rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0));
-          }
-          fv_t zv;
-#pragma unroll
-          for (int x = 0; x < MO; ++x) {
-            z[x] = y[yy][x] + bb;
-            if (p.res) z[x] += rv[x];
-            z[x] = (p.relu && z[x] < 0.0f) ? 0.0f : z[x];
-            zv[x] = z[x];
-          }
-          const uv_t v = __builtin_bit_cast(uv_t, zv);
-          if constexpr (MO == 4) {
-            if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_SC1);
-            else __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_OUT);
-          } else {
-            if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_SC1);
-            else __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_OUT);
-          }
-          continue;
-        }
+        fv_t zv;
 #pragma unroll
         for (int x = 0; x < MO; ++x) {
-          const bool in = ok & (oy0 + yy < p.OH) & (ox0 + x < p.OW);
-          const uint32_t off = oob_unless(in, (ob + yy * p.OW + x) * 4u);
-          float z = y[yy][x] + bb;
-          if (p.res) z += ld1(rsr, off);
-          z = (p.relu && z < 0.0f) ? 0.0f : z;
-          if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_SC1);
-          else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_OUT);
+          z[x] = y[yy][x] + bb;
+          if (p.res) z[x] += rv[x];
+          z[x] = (p.relu && z[x] < 0.0f) ? 0.0f : z[x];
+          zv[x] = z[x];
+        }
+        const uv_t v = __builtin_bit_cast(uv_t, zv);
+        if constexpr (MO == 4) {
+          if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_SC1);
+          else __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_OUT);
+        } else {
+          if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_SC1);
+          else __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_OUT);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int x = 0; x < MO; ++x) {
+        const bool in = ok & (oy0 + yy < p.OH) & (ox0 + x < p.OW);
+        const uint32_t off = oob_unless(in, (ob + yy * p.OW + x) * 4u);
+        float z = y[yy][x] + bb;
+        if (p.res) z += ld1(rsr, off);
+        z = (p.relu && z < 0.0f) ? 0.0f : z;
+        if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_OUT);
+      }
+    }
+  };
+
+  f32x16 acc[PPG];
+  const uint32_t tfirst = fdiv(it0, p.ipt_m, p.ipt_s);  // the block's first unit (slab slot 0)
+  // one run: stages sa .. sb - 1 of unit t (SK = 0: the whole unit, once)
+  auto run = [&](uint32_t t, uint32_t sa, bool first_run) {
+    setup_unit(t);
+#pragma unroll
+    for (int q = 0; q < PPG; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
+
+    // ---- prologue: strips of stages sa and sa + 1, then U(sa) (still in flight while V(sa) is made:
+    // the loop's first waits count on exactly the steady state's [strip][U k0][U k1] order)
+    issue_strip(0, sa);
+    issue_strip(1, sa + 1);
+    load_u(0, sa);
+    load_u(1, sa);
+    vm_wait<2 * NLU>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // (also: every wave past the previous run's last LDS reads)
+    asm volatile("" ::: "memory");
+    transform(0, 0);
+    if (first_run) KT(1);
+
+    // per stage and lane, VMEM in issue order: strip(it + 2) (SP DMAs) right after the barrier, then
+    // U(it + 1) k step 0 (NLU loads) after the k-step-0 MFMAs, U(it + 1) k step 1 (NLU) at the end.
+    // Top of stage it: strip(it + 1) must have landed -> vmcnt(2 NLU); before k step 0's MFMAs U(it)
+    // step 0 -> vmcnt(NLU + SP); before k step 1's, U(it) step 1 -> vmcnt(SP + NLU)
+    for (uint32_t s = sa; s < sb; ++s) {
+      const int vb = (int)((s - sa) & 1u);
+      vm_wait<2 * NLU>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr ((DBG & 32) == 0) __builtin_amdgcn_s_barrier();  // V(s) written, strip(s + 1) landed, strip(s)'s slot free
+      asm volatile("" ::: "memory");
+      if constexpr ((DBG & 4) == 0) issue_strip(vb, s + 2);
+      else if constexpr ((DBG & 64) == 0) issue_strip(vb, sb);  // dead: the same VMEM count, no memory touched
+      if constexpr ((DBG & 16) == 0) {
+        load_vf(vb, 0);
+        load_vf(vb, 1);
+      }
+      // strip(s + 1) -> V(s + 1) in three phases around the MFMA groups (its reads land under them)
+      constexpr bool XF = (DBG & 1) == 0;
+      if (XF && xf) tx_read(vb ^ 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<NLU + SP>();
+#pragma unroll
+      for (int q = 0; q < PPG; ++q) {
+        if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+        else asm volatile("" ::"v"(ur[0][q]), "v"(vf[0][q]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((DBG & 8) == 0) load_u(0, s + 1);
+      else if constexpr ((DBG & 128) == 0) load_u(0, sb);  // dead loads (misses): the same VMEM count
+      if (XF && xf) {
+        tx_e(0);
+        if constexpr (N == 6) tx_read(vb ^ 1, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<SP + NLU>();
+#pragma unroll
+      for (int q = 0; q < PPG; ++q) {
+        if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+        else asm volatile("" ::"v"(ur[1][q]), "v"(vf[1][q]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((DBG & 8) == 0) load_u(1, s + 1);
+      else if constexpr ((DBG & 128) == 0) load_u(1, sb);
+      if (XF && xf) {
+        if constexpr (N == 6) tx_e(1);
+        tx_v(vb ^ 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave done with the strips and V: the LDS is the exchange now
+    asm volatile("" ::: "memory");
+    if (first_run) KT(2);
+
+    // ---- epilogue: rounds of ECH accumulator elements
+    const bool whole = !SK || (sa == 0 && sb == ipt);  // uniform
+    const uint32_t rtile = g0 + (rlane & 31u);
+    const bool tvalid = rtile < p.T;
+    // this thread's bias values of every round, loaded before the first round (one memory latency,
+    // not one per round)
+    float rbias[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const uint32_t ee = (uint32_t)(r * ECH) + rel;
+      const uint32_t oc = oc0 + rog * 32u + 8u * (ee >> 2) + 4u * (rlane >> 5) + (ee & 3u);
+      rbias[r] = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+    }
+    uint32_t obase = 0, oy0 = 0, ox0 = 0;
+    {
+      const uint32_t tg = tvalid ? rtile : 0u;
+      const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+      const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+      oy0 = MO * ty;
+      ox0 = MO * tx;
+      obase = img * p.OCOHW + oy0 * p.OW + ox0;
+    }
+    // a cut unit's partial outputs (after the transform, before the bias) go to this block's slab:
+    // slot 0 for its first unit, 1 for its last ([round][thread][MO x MO], write-through)
+    const uint32_t sl = t == tfirst ? 0u : 1u;
+    const __amdgpu_buffer_rsrc_t rws =
+        make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (size_t)(NR * XNT * MM), NR * XNT * MM * 4);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int r0 = r * ECH;
+      // write: this wave's PPG values of elements r0 .. r0 + ECH - 1
+#pragma unroll
+      for (int el = 0; el < ECH; ++el) {
+        float m[PPG];
+#pragma unroll
+        for (int q = 0; q < PPG; ++q) m[q] = acc[q][r0 + el];
+        float *const dst = xb + ((og * ECH + el) * 64 + lane) * XS + pg * PS;
+        *(f32x4v *)dst = f32x4v{m[0], m[1], m[2], m[3]};
+        *(f32x4v *)(dst + 4) = f32x4v{m[4], m[5], m[6], m[7]};
+        if constexpr (N == 6) dst[8] = m[8];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // read: the pair's N x N values, A^T M A, then store (or the partial to the slab)
+      {
+        float mm[N][N];
+        const float *const src = xb + (size_t)tid * XS;
+#pragma unroll
+        for (int g = 0; g < NPG; ++g) {
+          float m[PPG];
+          const f32x4v a = *(const f32x4v *)(src + g * PS), b = *(const f32x4v *)(src + g * PS + 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            m[q] = a[q];
+            m[4 + q] = b[q];
+          }
+          if constexpr (N == 6) m[8] = src[g * PS + 8];
+#pragma unroll
+          for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+              if (wx_group<N>(i, j) == g) mm[i][j] = m[wx_slot<N>(i, j)];
+        }
+        float tt[N][MO];  // T = M A (each row of M through A^T)
+#pragma unroll
+        for (int i = 0; i < N; ++i) at_row<MO, N>(mm[i], tt[i]);
+        float y[MO][MO];  // Y = A^T T (each column of T)
+#pragma unroll
+        for (int x = 0; x < MO; ++x) {
+          float col[N], o[MO];
+#pragma unroll
+          for (int i = 0; i < N; ++i) col[i] = tt[i][x];
+          at_row<MO, N>(col, o);
+#pragma unroll
+          for (int yy = 0; yy < MO; ++yy) y[yy][x] = o[yy];
+        }
+        if (whole) {
+          store_y(r, y, rbias[r], tvalid, obase, oy0, ox0);
+        } else if constexpr (SK) {
+#pragma unroll
+          for (int q = 0; q < MM; q += 4) {
+            const f32x4v v = {y[q / MO][q % MO], y[(q + 1) / MO][(q + 1) % MO], y[(q + 2) / MO][(q + 2) % MO],
+                              y[(q + 3) / MO][(q + 3) % MO]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                   rws, (uint32_t)(((r * XNT + tid) * MM + q) * 4), 0, AUX_SC1);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every reader done before the next round's writes
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (SK) {
+      if (!whole) {
+        // the unit's blocks b0 .. b1 (in block order); the last to arrive sums their partials
+        const uint32_t b0 = (t * ipt) / p.ipb, b1 = (t * ipt + ipt - 1) / p.ipb;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        uint32_t *const flag = (uint32_t *)(smem + FLAG);
+        if (tid == 0) {
+          const uint32_t old = __hip_atomic_fetch_add(&p.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t last = old == b1 - b0 ? 1u : 0u;
+          if (last) __hip_atomic_store(&p.cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flag = last;
+        }
+        __syncthreads();
+        if (*flag) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+          const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+          float ys[NR][MM];
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int q = 0; q < MM; ++q) ys[r][q] = 0.0f;
+          for (uint32_t b = b0; b <= b1; ++b) {  // block order = k order: bitwise reproducible
+            const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+            const uint32_t base = (b * 2 + s2) * (uint32_t)(NR * XNT * MM * 4);
+            f32x4v x[NR][MM / 4];
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+              for (int q = 0; q < MM / 4; ++q)
+                x[r][q] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rall, base + (uint32_t)(((r * XNT + tid) * MM + 4 * q) * 4), 0,
+                                                         AUX_SC1));
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+              for (int q = 0; q < MM / 4; ++q)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ys[r][4 * q + c] += x[r][q][c];
+          }
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            float y[MO][MO];
+#pragma unroll
+            for (int q = 0; q < MM; ++q) y[q / MO][q % MO] = ys[r][q];
+            store_y(r, y, rbias[r], tvalid, obase, oy0, ox0);
+          }
         }
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every reader done before the next round's writes
-    asm volatile("" ::: "memory");
+  };
+  if constexpr (SK) {
+    bool first_run = true;
+    for (uint32_t it = it0; it < it1;) {
+      const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
+      sb = min(ipt, it1 - t * ipt);
+      run(t, it - t * ipt, first_run);
+      first_run = false;
+      it = t * ipt + sb;
+    }
+  } else {
+    sb = ipt;
+    run(lb, 0u, true);
   }
   vm_wait<0>();
   KT(4);
 }
 
-template <int MO, int R, int SP, int NW, int DBG = 0>
+template <int MO, int R, int SP, int NW, int DBG = 0, int SK = 0>
 cfg_t wgx_cfg(const char *name) {
   using G = wx_geom<MO, R, NW>;
   cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, DBG>;
+  c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, SK, DBG>;
+  c.dc_wpm = SK;  // (dc == 5) persistent stream-K grid
   c.dc = 5;
   c.dc_ky = R;
   c.dc_kx = R;
@@ -627,13 +727,23 @@ std::vector<cfg_t> wgx_cfgs() {
   // <MO, R, SP, NW>: output tile MO x MO, filter R x R (patch MO + R - 1), SP dword strip DMAs per
   // lane and stage (the strip [4][RIN][WPM] must fit SP * 64 NW floats), NW waves per block
   return {
-      wgx_cfg<4, 3, 4, 8>("wx43s4"),   wgx_cfg<4, 3, 8, 8>("wx43s8"),   wgx_cfg<4, 3, 12, 8>("wx43s12"),
-      wgx_cfg<2, 5, 3, 8>("wx25s3"),   wgx_cfg<2, 5, 6, 8>("wx25s6"),   wgx_cfg<2, 5, 10, 8>("wx25s10"),
-      wgx_cfg<2, 3, 3, 8>("wx23s3"),   wgx_cfg<2, 3, 6, 8>("wx23s6"),   wgx_cfg<2, 3, 10, 8>("wx23s10"),
+      // (a dead DMA instruction costs about what a live one does: SP close to the strip's need)
+      wgx_cfg<4, 3, 4, 8>("wx43s4"),   wgx_cfg<4, 3, 8, 8>("wx43s8"),   wgx_cfg<4, 3, 9, 8>("wx43s9"),
+      wgx_cfg<4, 3, 10, 8>("wx43s10"), wgx_cfg<4, 3, 12, 8>("wx43s12"),
+      wgx_cfg<2, 5, 3, 8>("wx25s3"),   wgx_cfg<2, 5, 4, 8>("wx25s4"),   wgx_cfg<2, 5, 5, 8>("wx25s5"),
+      wgx_cfg<2, 5, 6, 8>("wx25s6"),   wgx_cfg<2, 5, 10, 8>("wx25s10"),
+      wgx_cfg<2, 3, 2, 8>("wx23s2"),   wgx_cfg<2, 3, 3, 8>("wx23s3"),   wgx_cfg<2, 3, 4, 8>("wx23s4"),
+      wgx_cfg<2, 3, 6, 8>("wx23s6"),   wgx_cfg<2, 3, 10, 8>("wx23s10"),
       // four waves (OC tile 32 / 64): twice the units, two blocks per CU -- the small-batch shapes
-      wgx_cfg<4, 3, 8, 4>("wx43s8w4"), wgx_cfg<4, 3, 16, 4>("wx43s16w4"),
-      wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
-      wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
+      wgx_cfg<4, 3, 8, 4>("wx43s8w4"), wgx_cfg<4, 3, 12, 4>("wx43s12w4"), wgx_cfg<4, 3, 16, 4>("wx43s16w4"),
+      wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 8, 4>("wx25s8w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
+      wgx_cfg<2, 3, 4, 4>("wx23s4w4"), wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 8, 4>("wx23s8w4"),
+      wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
+      // stream-K grids (F(2x2, 3x3) only: a cut unit's partial outputs are 4 floats per channel-tile pair)
+      wgx_cfg<2, 3, 2, 8, 0, 1>("wx23s2k"), wgx_cfg<2, 3, 3, 8, 0, 1>("wx23s3k"), wgx_cfg<2, 3, 4, 8, 0, 1>("wx23s4k"),
+      wgx_cfg<2, 3, 6, 8, 0, 1>("wx23s6k"),
+      wgx_cfg<2, 3, 4, 4, 0, 1>("wx23s4w4k"), wgx_cfg<2, 3, 6, 4, 0, 1>("wx23s6w4k"), wgx_cfg<2, 3, 8, 4, 0, 1>("wx23s8w4k"),
+      // (F(2x2, 5x5) stream-K forms spill registers (8-56 VGPRs): not built)
 #ifdef BH_KTRACE
       // diagnostic builds of wx43s12 / wx25s6 (wrong results by design): one part of the stage dropped
       wgx_cfg<4, 3, 12, 8, 1>("xwx43_noxf"), wgx_cfg<4, 3, 12, 8, 2>("xwx43_nomfma"),
@@ -714,24 +824,46 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   p.ngr = ngroups;
   f = bh::make_fastdiv(ngroups); p.ngr_m = f.m; p.ngr_s = f.s;
   p.ipt = IC / XC;
+  f = bh::make_fastdiv(p.ipt); p.ipt_m = f.m; p.ipt_s = f.s;
   p.relu = relu;
   p.wt = wt;
   p.vst = (OW % MO == 0 && ((uintptr_t)out % (4 * MO)) == 0 && ((uintptr_t)res % (4 * MO)) == 0) ? 1 : 0;
   const uint32_t OCT = (uint32_t)c.BM, octiles = (OC + OCT - 1) / OCT;
   const uint64_t units = (uint64_t)ngroups * octiles;
   if (units >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many Winograd units");
-  // dynamic LDS: two strip slots + two V buffers, or the epilogue's exchange (512 pairs x pitch)
+  // dynamic LDS: two strip slots + two V buffers, or the epilogue's exchange (NT pairs x pitch); then
+  // the stream-K ticket flag
   const uint32_t NPG = N == 6 ? 4 : 2, PS = N == 6 ? 12 : 8, XS = N == 6 ? 52 : 20;
-  const uint32_t lds = std::max(2 * SP * XNT + 2 * NPG * XC * XTT * PS, XNT * XS) * 4;
+  const uint32_t lds = (std::max(2 * SP * XNT + 2 * NPG * XC * XTT * PS, XNT * XS) + 4) * 4;
   if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: LDS too small for ") + c.name);
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
+  uint32_t G = (uint32_t)units;
+  if (c.dc_wpm) {
+    // stream-K: as many blocks as are resident at once, the (unit, stage) iterations dealt equally
+    if (MO != 2) return bh::fail(BH_UNSUP, "conv: stream-K Winograd is for the 2x2-output forms");
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)XNT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+    const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+    const uint64_t total = units * p.ipt;
+    if (total >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many Winograd iterations");
+    const uint64_t g = (uint64_t)ncu * (uint32_t)std::min(occ, 2);
+    p.ipb = (uint32_t)((total + g - 1) / g);
+    G = (uint32_t)((total + p.ipb - 1) / p.ipb);
+    p.total_it = (uint32_t)total;
+    const size_t slab = (size_t)(16 / (XNT / ((XNT / 64 / NPG) * 64))) * XNT * MO * MO;  // NR * NT * MO^2 floats
+    int rc = ensure_ws(ctx, (size_t)2 * G * slab * 4);
+    if (rc == BH_OK) rc = ensure_cnt(ctx, units);
+    if (rc != BH_OK) return rc;
+    p.ws = (float *)ctx->ws;
+    p.cnt = (uint32_t *)ctx->cnt;
+  }
 #ifdef BH_KTRACE
   p.trace = (unsigned long long *)ctx->stamps + 65536;
 #endif
   void *args[] = {&p};
-  return bh::launch(ctx, k, dim3((uint32_t)units, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
+  return bh::launch(ctx, k, dim3(G, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
 }
 
 }  // namespace bhk

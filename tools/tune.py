@@ -168,7 +168,7 @@ def main():
                         if kind == 1 and s.KY == s.KX == 3 and s.sy == s.sx == 1 and s.py <= 1 and s.px <= 1:
                             cand += [(ci, 1), (ci, 5), (ci, 11), (ci, 15)]  # one block per CU (256 AGPRs)
                         continue
-                    if cn.startswith("wx"):  # position-split Winograd: whole units; UNSUP for other ops
+                    if cn.startswith("wx"):  # position-split Winograd (planned grid); UNSUP for other ops
                         r = 5 if cn.startswith("wx25") else 3
                         if kind == 1 and s.KY == s.KX == r and s.sy == s.sx == 1 and s.py == s.px <= r // 2:
                             cand.append((ci, 0))
