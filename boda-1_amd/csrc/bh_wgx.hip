@@ -177,7 +177,6 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   };
 
   const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.in, p.in_bytes);
-  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(p.in, 0u);
   const __amdgpu_buffer_rsrc_t rsu = make_rsrc(p.u, p.u_bytes);
 
   // ---- per-unit state (setup_unit): the unit's OC tile and tile group, the strip DMA plan (per
@@ -233,10 +232,12 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     }
   };
   auto issue_strip = [&](int slot, uint32_t it) {  // stage it's strip (dead past the run: no memory touched)
+    // (a dead stage's offsets all miss; selecting between two resources instead put both in scratch
+    // and reloaded one per stage)
     const bool live = it < sb;
-    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u;
+    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u, dead = live ? 0u : OOB;
 #pragma unroll
-    for (int j = 0; j < SP; ++j) dma4s(live ? rsi : rnull, smem + slot * SCAP + j * XNT + tid, svo[j], ss);
+    for (int j = 0; j < SP; ++j) dma4s(rsi, smem + slot * SCAP + j * XNT + tid, svo[j] | dead, ss);
   };
   float ur[2][PPG];
   auto load_u = [&](int s, uint32_t it) {
@@ -739,11 +740,13 @@ std::vector<cfg_t> wgx_cfgs() {
       wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 8, 4>("wx25s8w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
       wgx_cfg<2, 3, 4, 4>("wx23s4w4"), wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 8, 4>("wx23s8w4"),
       wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
-      // stream-K grids (F(2x2, 3x3) only: a cut unit's partial outputs are 4 floats per channel-tile pair)
+      // stream-K grids (F(2x2, .) only: a cut unit's partial outputs are 4 floats per channel-tile pair)
       wgx_cfg<2, 3, 2, 8, 0, 1>("wx23s2k"), wgx_cfg<2, 3, 3, 8, 0, 1>("wx23s3k"), wgx_cfg<2, 3, 4, 8, 0, 1>("wx23s4k"),
       wgx_cfg<2, 3, 6, 8, 0, 1>("wx23s6k"),
       wgx_cfg<2, 3, 4, 4, 0, 1>("wx23s4w4k"), wgx_cfg<2, 3, 6, 4, 0, 1>("wx23s6w4k"), wgx_cfg<2, 3, 8, 4, 0, 1>("wx23s8w4k"),
-      // (F(2x2, 5x5) stream-K forms spill registers (8-56 VGPRs): not built)
+      // (the F(2x2, 5x5) forms spill ~20 loop-invariant VGPRs, reloaded once per unit run)
+      wgx_cfg<2, 5, 3, 8, 0, 1>("wx25s3k"), wgx_cfg<2, 5, 4, 8, 0, 1>("wx25s4k"), wgx_cfg<2, 5, 6, 8, 0, 1>("wx25s6k"),
+      wgx_cfg<2, 5, 6, 4, 0, 1>("wx25s6w4k"), wgx_cfg<2, 5, 8, 4, 0, 1>("wx25s8w4k"), wgx_cfg<2, 5, 12, 4, 0, 1>("wx25s12w4k"),
 #ifdef BH_KTRACE
       // diagnostic builds of wx43s12 / wx25s6 (wrong results by design): one part of the stage dropped
       wgx_cfg<4, 3, 12, 8, 1>("xwx43_noxf"), wgx_cfg<4, 3, 12, 8, 2>("xwx43_nomfma"),
