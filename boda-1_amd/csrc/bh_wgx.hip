@@ -232,12 +232,15 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     }
   };
   auto issue_strip = [&](int slot, uint32_t it) {  // stage it's strip (dead past the run: no memory touched)
-    // (a dead stage's offsets all miss; selecting between two resources instead put both in scratch
-    // and reloaded one per stage)
+    // Everything here is scalar: a dead stage reads through a descriptor with no records (selecting
+    // between two descriptor variables instead put both in scratch and reloaded one per stage; a
+    // per-lane miss mask cost one VALU op per DMA), and the LDS destination is the wave's base (a
+    // per-lane address costs a VALU add and a readfirstlane per DMA)
     const bool live = it < sb;
-    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u, dead = live ? 0u : OOB;
+    const uint32_t ss = live ? it * XC * p.HW * 4u : 0u;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.in, live ? p.in_bytes : 0u);
 #pragma unroll
-    for (int j = 0; j < SP; ++j) dma4s(rsi, smem + slot * SCAP + j * XNT + tid, svo[j] | dead, ss);
+    for (int j = 0; j < SP; ++j) dma4s(rs, smem + slot * SCAP + j * XNT + wave * 64, svo[j], ss);
   };
   float ur[2][PPG];
   auto load_u = [&](int s, uint32_t it) {
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   // reads patch rows 3h .. 3h + 2 (4x4: all four rows at h = 0), tx_e(h) makes their E = d B values,
   // tx_v makes V = B^T E from the whole E and writes it (NW = 8 leaves waves 4..7 without patches;
   // the callers test xf, which is wave-uniform)
-  const bool xf = tid < 256;
+  const bool xf = wave < 4;  // (uniform: a branch, not an exec mask)
   constexpr int NRD = N == 6 ? 3 : 4, NCE = N == 6 ? 3 : 4;
   float dr[NRD][N];
   float e[N][NCE];
@@ -740,10 +743,12 @@ std::vector<cfg_t> wgx_cfgs() {
       wgx_cfg<2, 5, 6, 4>("wx25s6w4"), wgx_cfg<2, 5, 8, 4>("wx25s8w4"), wgx_cfg<2, 5, 12, 4>("wx25s12w4"),
       wgx_cfg<2, 3, 4, 4>("wx23s4w4"), wgx_cfg<2, 3, 6, 4>("wx23s6w4"), wgx_cfg<2, 3, 8, 4>("wx23s8w4"),
       wgx_cfg<2, 3, 12, 4>("wx23s12w4"),
-      // stream-K grids (F(2x2, .) only: a cut unit's partial outputs are 4 floats per channel-tile pair)
+      // stream-K grids: a cut unit's partial outputs (MO x MO floats per channel-tile pair) go through a slab
       wgx_cfg<2, 3, 2, 8, 0, 1>("wx23s2k"), wgx_cfg<2, 3, 3, 8, 0, 1>("wx23s3k"), wgx_cfg<2, 3, 4, 8, 0, 1>("wx23s4k"),
       wgx_cfg<2, 3, 6, 8, 0, 1>("wx23s6k"),
       wgx_cfg<2, 3, 4, 4, 0, 1>("wx23s4w4k"), wgx_cfg<2, 3, 6, 4, 0, 1>("wx23s6w4k"), wgx_cfg<2, 3, 8, 4, 0, 1>("wx23s8w4k"),
+      // (F(4x4, 3x3): ~45 VGPRs spilled, all reloaded outside the stage loop)
+      wgx_cfg<4, 3, 10, 8, 0, 1>("wx43s10k"), wgx_cfg<4, 3, 12, 8, 0, 1>("wx43s12k"),
       // (the F(2x2, 5x5) forms spill ~20 loop-invariant VGPRs, reloaded once per unit run)
       wgx_cfg<2, 5, 3, 8, 0, 1>("wx25s3k"), wgx_cfg<2, 5, 4, 8, 0, 1>("wx25s4k"), wgx_cfg<2, 5, 6, 8, 0, 1>("wx25s6k"),
       wgx_cfg<2, 5, 6, 4, 0, 1>("wx25s6w4k"), wgx_cfg<2, 5, 8, 4, 0, 1>("wx25s8w4k"), wgx_cfg<2, 5, 12, 4, 0, 1>("wx25s12w4k"),
@@ -776,7 +781,8 @@ int launch_wx_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint3
 // Launch a position-split Winograd configuration: UNSUP unless a stride-1 R x R conv (R = the
 // configuration's) with pad <= R / 2, IC % 4 == 0, IC <= 512 for the 6x6 forms (their fp32
 // transform error), whose strips fit the configuration's slot. u: the bank of the configuration's
-// form (6x6: wx_pack; 4x4: bh_wino.hip's). One block per unit (whole units, no split).
+// form (6x6: wx_pack; 4x4: bh_wino.hip's). One block per unit (whole units), or (dc_wpm) a resident
+// stream-K grid over the (unit, stage) iterations.
 int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
                float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
@@ -845,7 +851,7 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   uint32_t G = (uint32_t)units;
   if (c.dc_wpm) {
     // stream-K: as many blocks as are resident at once, the (unit, stage) iterations dealt equally
-    if (MO != 2) return bh::fail(BH_UNSUP, "conv: stream-K Winograd is for the 2x2-output forms");
+    
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)XNT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
     const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
