@@ -33,11 +33,57 @@ constexpr int dc_koff(int tap, int KK) {
   return tap < KK ? (tap / KX) * WPM + tap % KX : 0;  // padding taps (zero weights): any in-strip offset
 }
 
+// Phase-split strip (PSL): strip column c = S * i + f sits at f * (WPM / S) + i, so the 32 pixels of a
+// fragment, S columns apart in the input, read 32 consecutive dwords (conflict-free) instead of
+// falling on 32 / S banks. Tap (ky, kx) of a pixel is at its base + dc_koffp(tap).
+template <int KX, int S, int WPM>
+constexpr int dc_koffp(int tap, int KK) {
+  return tap < KK ? (tap / KX) * WPM + ((tap % KX) % S) * (WPM / S) + (tap % KX) / S : 0;
+}
+// Lane half 1 reads tap KK2 + s where half 0 reads tap s; in the phase-split strip their offsets
+// differ by one of a few constants (by the taps' column phases). dk[k]: the distinct differences,
+// kind[s]: step s's.
+template <int KY, int KX, int S, int WPM>
+struct dc_pkinds {
+  static constexpr int KK = KY * KX, KK2 = (KK + 1) / 2;
+  struct tab_t {
+    int nk;
+    int dk[32];
+    int kind[KK2];
+  };
+  static constexpr tab_t make() {
+    tab_t t{};
+    for (int s = 0; s < KK2; ++s) {
+      const int d = dc_koffp<KX, S, WPM>(KK2 + s, KK) - dc_koffp<KX, S, WPM>(s, KK);
+      int k = -1;
+      for (int i = 0; i < t.nk; ++i)
+        if (t.dk[i] == d) k = i;
+      if (k < 0) {
+        k = t.nk;
+        t.dk[t.nk++] = d;
+      }
+      t.kind[s] = k;
+    }
+    return t;
+  }
+  static constexpr tab_t tab = make();
+};
+
+// compile-time loop: f(integral_constant<int, I>) for I in [I0, N) (hipcc leaves a long loop with many
+// per-step constants rolled, and the constants then index register arrays dynamically: scratch)
+template <int I, int N, class F>
+__device__ __forceinline__ void dc_static_for(F &&f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    dc_static_for<I + 1, N>(f);
+  }
+}
+
 // V4: input rows of W % 4 == 0 go into the strip as 16-B pieces (a quarter of the DMA
 // instructions: the strip's dword DMAs were 0.34 issues per MFMA at 11x11 s4); column c of the
 // strip then holds input x = c - PXA with PXA = 4 (0 without horizontal padding), so pieces start
 // on 16-B input boundaries
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0>
 __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int NW = 4;
   constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
@@ -48,6 +94,8 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int SF = RIN * WPM;
   constexpr int PW = V4 ? 4 : 1;                          // floats per strip DMA lane
   static_assert(WPM % PW == 0, "16-B strip rows");
+  static_assert(!PSL || (!V4 && WPM % S == 0), "phase-split strip: dword DMA, whole phases per row");
+  constexpr int WS = WPM / S;                             // PSL: strip floats per column phase
   constexpr int LWB = (SF / PW + NW * 64 - 1) / (NW * 64);  // strip DMA instructions per wave
   constexpr int SREG = LWB * NW * 64 * PW;
   constexpr int BREG = NW * 64;                           // the stage tile's biases, one DMA per wave
@@ -102,7 +150,8 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #pragma unroll
   for (int j = 0; j < LWB; ++j) {
     const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane) * PW;  // first strip element of the lane
-    const uint32_t r = e / WPM, c = e - (e / WPM) * WPM;
+    const uint32_t r = e / WPM, q = e - (e / WPM) * WPM;
+    const uint32_t c = PSL ? (q % WS) * S + q / WS : q;  // PSL: LDS position q holds column c
     const int x = (int)c - (int)pxa;
     // V4: a piece is inside the row or outside it as a whole (W % 4 == 0, pxa % 4 == 0)
     srow[j] = ((r < (uint32_t)RIN) & ((uint32_t)x < p.W)) ? r : 0xffffu;
@@ -180,6 +229,50 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     if (ic_issue == 0) plan_tile(i_issue);  // wave-uniform
     const float *const Ab = smem + slot * SLOT + kh * KK2 * OCT + li;
     const char *const Sb = (const char *)(smem + slot * SLOT + WREG);
+    if constexpr (PSL) {
+      // phase-split strip: one per-lane base per distinct half-1 shift (a handful), the step loop
+      // unrolled at compile time so that every fragment read is base[kind(s)] + immediate
+      using PK = dc_pkinds<KY, KX, S, WPM>;
+      constexpr int NK = PK::tab.nk;
+      asm volatile("" : "+v"(hsel));
+      const char *bs[NK][TN];
+      dc_static_for<0, NK>([&](auto kc) {
+        constexpr int dkv = PK::tab.dk[decltype(kc)::value];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) bs[decltype(kc)::value][tn] = Sb + poff[tn] + (int)(hsel & (uint32_t)(dkv * 4));
+      });
+      auto fragp = [&](auto sc, float(&a)[TM], float(&b)[TN]) {
+        constexpr int s = decltype(sc)::value;
+        constexpr int k0 = dc_koffp<KX, S, WPM>(s, KK) * 4, kind = PK::tab.kind[s];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) a[t] = Ab[s * OCT + 32 * t];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) b[tn] = *(const float *)(bs[kind][tn] + k0);
+      };
+      float a[PF + 1][TM], b[PF + 1][TN];
+      dc_static_for<0, PF>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s < KK2) fragp(sc, a[s], b[s]);
+      });
+      dc_static_for<0, KK2>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s + PF < KK2) fragp(std::integral_constant<int, s + PF>{}, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[t][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)][tn], a[s % (PF + 1)][t], acc[t][tn], 0, 0, 0);
+#pragma unroll
+        for (int q = (s * LW + IS - 1) / IS; q < ((s + 1) * LW + IS - 1) / IS && q < LW; ++q) issue_one(q, islot, ic_issue);
+        if (dstores) {
+#pragma unroll
+          for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      return;
+    }
     // Lane half 1 reads tap KK2 + s where half 0 reads tap s: its strip offset is larger by
     // dk(s) = koff(KK2 + s) - koff(s), which takes only two values over the real taps (DLO while
     // the column shift KK2 % KX does not wrap, DHI when it does) and a third at the padding
@@ -256,7 +349,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
     for (int tn = 0; tn < TN; ++tn) {
       const uint32_t px = p0 + (uint32_t)(wave * 32 * TN + 32 * tn + li);
       const uint32_t oy = fdiv(px, p.ow_m, p.ow_s), ox = px - oy * p.OW;
-      poff[tn] = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S + pxa - p.px) * 4u : 0u;
+      poff[tn] = px < p.OHW ? ((oy - oy_a) * S * WPM + (PSL ? ox : ox * S) + pxa - p.px) * 4u : 0u;
     }
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -341,10 +434,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #endif
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0>
 cfg_t dc_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 128 * TN, 2 * ((KY * KX + 1) / 2), 256, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D, V4>;
+  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D, V4, PSL>;
   c.dc_ci = V4;  // dc == 1: 16-B strip pieces (input rows of W % 4 == 0)
   c.dc = 1;
   c.dc_ky = KY;
@@ -375,6 +468,12 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 1>("dc11s4x32d2v"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3, 1>("dc11s4x32d3v"),
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2, 1>("dc11s4x96d2v"),
+      // phase-split strips (conflict-free fragment reads; dword strip DMA)
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 0, 1>("dc11s4x32d2p"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 3, 0, 1>("dc11s4x32d3p"),
+      dc_cfg<11, 11, 4, 228, 23, 3, 1, 2, 0, 1>("dc11s4x96d2p"),
+      dc_cfg<7, 7, 2, 236, 11, 2, 1, 2, 0, 1>("dc7s2x64n128d2p"),
+      dc_cfg<7, 7, 2, 236, 13, 2, 2, 2, 0, 1>("dc7s2x64d2p"),
       // op_sigs' wide stems: 3 x 516^2 -> 96 11x11 s4 and 6x6 s2, 3 x 224^2 -> 96 11x11 s2
       dc_cfg<11, 11, 4, 516, 19, 1, 1, 2, 1>("dc11s4x32w516d2v"),
       dc_cfg<6, 6, 2, 516, 10, 1, 1, 3, 1>("dc6s2x32w516d3v"),

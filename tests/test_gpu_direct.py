@@ -6,7 +6,9 @@ it is forced with bh_tune_set on stem-like shapes of that kernel -- the conv set
 tiles that straddle output rows and images, asymmetric padding -- and checked against the
 double-accumulated oracle (tolerances of test_gpu_conv.py). Bits must not
 depend on whether the bank was packed up front, and the residual / channel-slab epilogues
-must equal the plain call's bits (what the net executor relies on).
+must equal the plain call's bits (what the net executor relies on). Configurations ending in "p"
+store the strip phase-split (column c at (c % S) * WPM / S + c / S) and read it through per-step
+compile-time bases.
 """
 import re
 
@@ -91,7 +93,7 @@ def test_direct_rejects_other_kernels(dev, cn):
         dev.tune_set(1, -1, 0)
 
 
-@pytest.mark.parametrize("cn", [DC[0], [n for n in DC if n.startswith("dc11")][0]])
+@pytest.mark.parametrize("cn", [DC[0], [n for n in DC if n.startswith("dc11")][0]] + [n for n in DC if n == "dc11s4x32d2p"])
 def test_direct_residual_and_slab(dev, cn):
     k, st = kernel_of(cn)
     s = SHAPES[(k, st)][1]  # a conv-set stem: fits every instantiation of its kernel

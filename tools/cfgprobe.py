@@ -48,6 +48,7 @@ def main():
         kind = 0 if isinstance(s, ops.SgemmShape) else 1
         wl = runner.Workload(dev, [s])
         dev.tune_set(kind, -1, 0)
+        tune.time_op(dev, wl, 0, 3)  # (the first timing of a process runs ~10 % slow: clocks, caches)
         t0 = tune.time_op(dev, wl, 0, 3)
         rf = runner.roofline_secs(s) * 1e3
         print("%s  tuned %.4f ms (%.0f%% roofline)" % (s, t0, 100 * rf / t0), flush=True)
