@@ -93,6 +93,29 @@ def time_op_flush(dev, wl, i, reps):
     return statistics.median(out)
 
 
+def write_table(args, plat, table, results):
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    lines = {k: "%s cfg=%s splits=%d red=%s%s" % (k, cn, abs(S), "k" if S < 0 else "i", " wt=1" if wt else "")
+             for k, (cn, S, t, td, wt) in table.items()}
+    if args.merge and os.path.exists(args.out):
+        old = {}
+        for l in open(args.out):
+            if l.startswith("#") or " cfg=" not in l:
+                continue
+            old[l[:l.index(" cfg=")]] = l.rstrip("\n")
+        old.update(lines)
+        lines = old
+    tmp = args.out + ".tmp"
+    with open(tmp, "w") as f:
+        f.write("# boda-1_amd tuning table (tools/tune.py) for %s; <op> <dims> cfg=<tile config> splits=<K splits>\n"
+                % plat)
+        for k in sorted(lines, key=lambda k: (k.split()[0], [int(x) for x in k.split()[1:]])):
+            f.write(lines[k] + "\n")
+    os.replace(tmp, args.out)
+    if args.json:
+        json.dump({"plat": plat, "results": results}, open(args.json, "w"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default="conv,sgemm-full,sgemm-small")
@@ -114,6 +137,12 @@ def main():
                     help="output store policy: try write-through (wt=1) on each op's best config and keep it if "
                          "faster by --wt-gain; 'only': keep the --out table's configs, sweep just the policy")
     ap.add_argument("--wt-gain", type=float, default=0.01)
+    ap.add_argument("--confirm", type=int, default=0, help="re-time the TOP fastest routes of the sweep (and the "
+                    "--out table's current choice) this many times each and pick by median: one timing per "
+                    "candidate picks the luckiest of many noisy draws")
+    ap.add_argument("--top", type=int, default=3)
+    ap.add_argument("--keep-prev", action="store_true", help="load the --out table's choices as with --cfg-re: "
+                    "kept unless beaten by --min-gain")
     args = ap.parse_args()
     global TIMING
     TIMING = args.timing
@@ -123,7 +152,7 @@ def main():
     names = {0: boda_hip.tune_cfg_names(0), 1: boda_hip.tune_cfg_names(1)}
     table, results = {}, []
     prev = {}
-    if (args.cfg_re or args.wt == "only") and os.path.exists(args.out):
+    if (args.cfg_re or args.wt == "only" or args.keep_prev) and os.path.exists(args.out):
         for l in open(args.out):
             m = re.match(r"(.*) cfg=(\S+) splits=(\d+) red=(\w)", l)
             if m:
@@ -210,7 +239,34 @@ def main():
                     best = (t, ci, S)
             dev.tune_set(kind, -1, 0)
             results.append({"key": key, "cfg": "default", "splits": 0, "ms": t_def})
-            if key in prev:  # keep the table's choice unless clearly beaten in this run
+            if args.confirm > 0:
+                # the TOP routes of the sweep and the table's choice, timed again: medians decide
+                mine = sorted([x for x in results if x["key"] == key and x["cfg"] != "default" and "wt" not in x],
+                              key=lambda x: x["ms"])
+                fin, seen = [], set()
+                for x in mine:
+                    k2 = (x["cfg"], x["splits"])
+                    if k2 not in seen and len(fin) < args.top:
+                        seen.add(k2)
+                        fin.append(k2)
+                if key in prev and prev[key] not in seen and prev[key][0] in names[kind]:
+                    fin.append(prev[key])
+                med = {}
+                for cn, S in fin:
+                    dev.tune_set(kind, names[kind].index(cn), S)
+                    try:
+                        med[(cn, S)] = statistics.median(time_op(dev, wl, 0, args.reps) for _ in range(args.confirm))
+                    except boda_hip.UnsupportedError:
+                        pass
+                dev.tune_set(kind, -1, 0)
+                for (cn, S), t in med.items():
+                    results.append({"key": key, "cfg": cn, "splits": S, "ms": t, "confirm": args.confirm})
+                if med:
+                    (cn, S), t = min(med.items(), key=lambda kv: kv[1])
+                    best = (t, names[kind].index(cn), S)
+                    if key in prev and prev[key] in med and t >= (1 - args.min_gain) * med[prev[key]]:
+                        best = (med[prev[key]], names[kind].index(prev[key][0]), prev[key][1])
+            elif key in prev:  # keep the table's choice unless clearly beaten in this run
                 pt = [x["ms"] for x in results if x["key"] == key and x["cfg"] == prev[key][0]
                       and x["splits"] == prev[key][1]]
                 if pt and best[0] >= (1 - args.min_gain) * pt[0]:
@@ -239,24 +295,9 @@ def main():
             print("%-48s default %.4f ms  best %s S=%+d %.4f ms  roofline %.4f ms (%.0f%%)" % (
                 key, t_def, names[kind][best[1]] if best[1] >= 0 else "default", best[2], best[0], rf,
                 100 * rf / best[0]), flush=True)
-    os.makedirs(os.path.dirname(args.out), exist_ok=True)
-    lines = {k: "%s cfg=%s splits=%d red=%s%s" % (k, cn, abs(S), "k" if S < 0 else "i", " wt=1" if wt else "")
-             for k, (cn, S, t, td, wt) in table.items()}
-    if args.merge and os.path.exists(args.out):
-        old = {}
-        for l in open(args.out):
-            if l.startswith("#") or " cfg=" not in l:
-                continue
-            old[l[:l.index(" cfg=")]] = l.rstrip("\n")
-        old.update(lines)
-        lines = old
-    with open(args.out, "w") as f:
-        f.write("# boda-1_amd tuning table (tools/tune.py) for %s; <op> <dims> cfg=<tile config> splits=<K splits>\n"
-                % plat)
-        for k in sorted(lines, key=lambda k: (k.split()[0], [int(x) for x in k.split()[1:]])):
-            f.write(lines[k] + "\n")
-    if args.json:
-        json.dump({"plat": plat, "results": results}, open(args.json, "w"))
+            if args.merge:  # written after every op: a sweep cut short by a time limit keeps its progress
+                write_table(args, plat, table, results)
+    write_table(args, plat, table, results)
     print("wrote %d entries to %s in %.0f s" % (len(table), args.out, time.time() - t_start))
     dev.close()
 
