@@ -87,6 +87,46 @@ __global__ __launch_bounds__(NW * 64) void fill_k(const float *buf, float *out, 
   if ((tid & 63) == 0) cyc[blockIdx.x * NW + (tid >> 6)] = t1 - t0;
 }
 
+// v_mfma_f32_16x16x4_f32 (half the flops of 32x32x2) with NACC independent accumulators, no fillers
+template <int NW, int NACC>
+__global__ __launch_bounds__(NW * 64) void m16_k(const float *buf, float *out, unsigned long long *cyc) {
+  const int tid = threadIdx.x;
+  f32x4 acc[NACC];
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float a = buf[tid], b = buf[tid + 64];
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < ITER; ++it) {
+#pragma unroll
+    for (int j = 0; j < NACC; ++j) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(a), "v"(b));
+  }
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  float sum = 0.0f;
+#pragma unroll
+  for (int j = 0; j < NACC; ++j) {
+    float v;
+    asm volatile("s_nop 7\n s_nop 7\n v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(acc[j][0]));
+    sum += v;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * NW * 64 + tid] = sum;
+  if ((tid & 63) == 0) cyc[blockIdx.x * NW + (tid >> 6)] = t1 - t0;
+}
+
+template <int NW, int NACC>
+int run16(const char *name, const float *buf, float *out, unsigned long long *cyc) {
+  const int blocks = 256;
+  for (int rep = 0; rep < 3; ++rep) m16_k<NW, NACC><<<blocks, NW * 64>>>(buf, out, cyc);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> h((size_t)blocks * NW);
+  CK(hipMemcpy(h.data(), cyc, h.size() * 8, hipMemcpyDeviceToHost));
+  std::sort(h.begin(), h.end());
+  std::printf("%-14s waves/SIMD %d  NACC %2d  16x16x4          : %6.1f cyc per MFMA\n", name, NW / 4, NACC,
+              (double)h[h.size() / 2] / (ITER * NACC));
+  return 0;
+}
+
 template <int NW, int NACC, int KIND, int F>
 int run(const char *name, const float *buf, float *out, unsigned long long *cyc) {
   const int blocks = 256;
@@ -109,6 +149,11 @@ int main() {
   CK(hipMalloc(&out, 256 * 512 * 4));
   CK(hipMalloc(&cyc, 256 * 8 * 8));
   int rc = 0;
+  rc |= run16<4, 1>("m16", buf, out, cyc);
+  rc |= run16<4, 4>("m16", buf, out, cyc);
+  rc |= run16<4, 8>("m16", buf, out, cyc);
+  rc |= run16<4, 16>("m16", buf, out, cyc);
+  rc |= run16<8, 8>("m16", buf, out, cyc);
   rc |= run<4, 16, K_NONE, 0>("none", buf, out, cyc);
   rc |= run<4, 1, K_NONE, 0>("none-dep", buf, out, cyc);
   rc |= run<4, 2, K_NONE, 0>("none-2acc", buf, out, cyc);
