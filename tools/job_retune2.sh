@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 cp boda-1_amd/tuning/gfx950.tune gpurun_out/tune.out
 export TMPDIR=/tmp
 timeout -k 10 ${TUNE_SECS:-1000} python -u tools/tune.py --sets ${SETS:-conv,op-sigs} --key-re "$KEY_RE" --merge \
-  --keep-prev --confirm 3 --min-gain 0.02 --out gpurun_out/tune.out --json gpurun_out/tune_rt.json \
+  --keep-prev --confirm 3 --min-gain ${MIN_GAIN:-0.02} ${TUNE_ARGS:-} --out gpurun_out/tune.out --json gpurun_out/tune_rt.json \
   > gpurun_out/tune_rt.log 2>&1
 rc=$?
 echo "tune rc=$rc"; tail -3 gpurun_out/tune_rt.log

@@ -235,6 +235,8 @@ def main():
                 except boda_hip.UnsupportedError:
                     continue
                 results.append({"key": key, "cfg": names[kind][ci], "splits": S, "ms": t})
+                if t > 5.0:  # long ops: a progress line per candidate (a silent minute reads as a hang)
+                    print("   %s S=%+d %.4f ms" % (names[kind][ci], S, t), flush=True)
                 if t < best[0]:
                     best = (t, ci, S)
             dev.tune_set(kind, -1, 0)
