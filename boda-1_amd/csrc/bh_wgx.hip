@@ -21,10 +21,13 @@
 //   Y = A^T M A (MO x MO outputs); points 0, 1, -1, 2, -2 (and infinity) for the 6x6 forms:
 //   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
 //   A^T (F43) = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1], A^T (F25) = its rows 0, 1
-//   with the last column of row 1 = 1. G is made on the host side of the pack kernel in double.
+//   with the last column of row 1 = 1. The pack kernel (wx_pack_kernel) makes G and G g G^T in double
+//   and rounds once.
 //
-// Structure (one fused kernel, nothing of U, V or M goes to HBM; one block per unit of OCT = 32 NOG
-// output channels x TT = 32 Winograd tiles of the flattened (image, tile row, tile column) space):
+// Structure (one fused kernel, nothing of U, V or M goes to HBM; a unit is OCT = 32 NOG output
+// channels x TT = 32 Winograd tiles of the flattened (image, tile row, tile column) space; one block
+// per unit, or -- the wx*k configurations -- a resident stream-K grid dealing the (unit, stage)
+// iterations, a unit cut between blocks summed after the output transform by its last arriver):
 //  * U (the pack, untimed like Boda's xpose_filts, src/rtc_prof.cc:93-99) goes from L2 straight into
 //    registers, one stage ahead, group by group after the MFMAs that freed the registers;
 //  * the stage's input strip [4 channels][RIN virtual rows][WPM] (rows img*VH + iy + pad, columns
