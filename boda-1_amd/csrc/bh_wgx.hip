@@ -146,6 +146,8 @@ __device__ __forceinline__ uint32_t wx_lb(uint32_t bid, uint32_t G) {
 // SK = 0: one block per unit (whole units); SK = 1: a persistent stream-K grid dealing the (unit, stage)
 // iterations equally between the blocks; a unit cut between blocks is summed after the output
 // transform (linear) by its last-arriving block in block order (bitwise reproducible)
+// SK = 2: whole units in full rounds of resident blocks, the last partial round's units split into S
+// pieces along the stages (the same slab hand-off), so the tail runs S times shorter
 template <int MO, int R, int SP, int NW, int SK, int DBG = 0>
 __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   using G = wx_geom<MO, R, NW>;
@@ -165,12 +167,15 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   const int pg = wave % NPG, og = wave / NPG;
   KT(0);
   const int li = lane & 31, kh = lane >> 5;
-  const uint32_t lb = wx_lb(blockIdx.x, gridDim.x);
+  // (SK 2: the hardware's dispatch order itself -- the whole units go out first, spread over all
+  // XCDs, and the tail pieces fill the CUs as they free; the XCD-contiguous remap would hand some XCDs
+  // only whole units and others only pieces)
+  const uint32_t lb = SK == 2 ? blockIdx.x : wx_lb(blockIdx.x, gridDim.x);
   const uint32_t ipt = p.ipt;
   // this block's iterations: SK -- [lb * ipb, + ipb); else unit lb. OC tile slowest in the unit order:
   // an XCD's run of units shares few OC tiles' U slices
-  const uint32_t it0 = SK ? lb * p.ipb : lb * ipt;
-  const uint32_t it1 = SK ? min(p.total_it, it0 + p.ipb) : it0 + ipt;
+  const uint32_t it0 = SK == 1 ? lb * p.ipb : lb * ipt;
+  const uint32_t it1 = SK == 1 ? min(p.total_it, it0 + p.ipb) : it0 + ipt;
 
   auto tpos = [&](uint32_t tg, uint32_t &v, uint32_t &x) {  // virtual row, strip column of tile tg's patch
     const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
@@ -524,7 +529,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     }
     // a cut unit's partial outputs (after the transform, before the bias) go to this block's slab:
     // slot 0 for its first unit, 1 for its last ([round][thread][MO x MO], write-through)
-    const uint32_t sl = t == tfirst ? 0u : 1u;
+    const uint32_t sl = SK == 2 || t == tfirst ? 0u : 1u;  // (SK 2: one unit per block)
     const __amdgpu_buffer_rsrc_t rws =
         make_rsrc(p.ws + ((size_t)lb * 2 + sl) * (size_t)(NR * XNT * MM), NR * XNT * MM * 4);
 #pragma unroll
@@ -596,7 +601,9 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
     if constexpr (SK) {
       if (!whole) {
         // the unit's blocks b0 .. b1 (in block order); the last to arrive sums their partials
-        const uint32_t b0 = (t * ipt) / p.ipb, b1 = (t * ipt + ipt - 1) / p.ipb;
+        // (SK 2: tail unit t's S = total_it parts are blocks ipb + (t - ipb) S ..)
+        const uint32_t b0 = SK == 2 ? p.ipb + (t - p.ipb) * p.total_it : (t * ipt) / p.ipb;
+        const uint32_t b1 = SK == 2 ? b0 + p.total_it - 1u : (t * ipt + ipt - 1) / p.ipb;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         uint32_t *const flag = (uint32_t *)(smem + FLAG);
@@ -616,7 +623,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
 #pragma unroll
             for (int q = 0; q < MM; ++q) ys[r][q] = 0.0f;
           for (uint32_t b = b0; b <= b1; ++b) {  // block order = k order: bitwise reproducible
-            const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+            const uint32_t s2 = (SK == 1 && b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
             const uint32_t base = (b * 2 + s2) * (uint32_t)(NR * XNT * MM * 4);
             f32x4v x[NR][MM / 4];
 #pragma unroll
@@ -644,7 +651,19 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       }
     }
   };
-  if constexpr (SK) {
+  if constexpr (SK == 2) {
+    // data-parallel rounds + a split tail: blocks below ipb take their unit whole; the rest take
+    // part j of S = total_it of a tail unit (stages [j ipt / S, (j + 1) ipt / S)), so the last,
+    // partly filled round of units runs as S times as many shorter pieces
+    if (lb < p.ipb) {
+      sb = ipt;
+      run(lb, 0u, true);
+    } else {
+      const uint32_t j = lb - p.ipb, S = p.total_it, part = j % S;
+      sb = (part + 1) * ipt / S;
+      run(p.ipb + j / S, part * ipt / S, true);
+    }
+  } else if constexpr (SK == 1) {
     bool first_run = true;
     for (uint32_t it = it0; it < it1;) {
       const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
@@ -666,7 +685,7 @@ cfg_t wgx_cfg(const char *name) {
   using G = wx_geom<MO, R, NW>;
   cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
   c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, SK, DBG>;
-  c.dc_wpm = SK;  // (dc == 5) persistent stream-K grid
+  c.dc_wpm = SK;  // (dc == 5) 1: persistent stream-K grid, 2: whole units + a split tail
   c.dc = 5;
   c.dc_ky = R;
   c.dc_kx = R;
@@ -752,6 +771,11 @@ std::vector<cfg_t> wgx_cfgs() {
       wgx_cfg<2, 3, 4, 4, 0, 1>("wx23s4w4k"), wgx_cfg<2, 3, 6, 4, 0, 1>("wx23s6w4k"), wgx_cfg<2, 3, 8, 4, 0, 1>("wx23s8w4k"),
       // (F(4x4, 3x3) stream-K forms, measured and not kept: ~45 VGPRs spilled outside the stage loop,
       // 98 against 81 us on 20x64x56^2->192)
+      // whole units + a split tail round (SK 2). Measured: 1x96x63^2->256 5x5 37.4 -> 33.1 us, the
+      // batch-20 5x5 ops -1 %; F(4x4, 3x3) 20x64x56^2->192 80 -> 100 us (a tail piece writes and the
+      // last arriver reads a whole 16-float-per-pair partial output through the write-through slab),
+      // F(2x2, 3x3) no gain: those forms are not built
+      wgx_cfg<2, 5, 4, 8, 0, 2>("wx25s4t"), wgx_cfg<2, 5, 6, 8, 0, 2>("wx25s6t"),
       // (the F(2x2, 5x5) forms spill ~20 loop-invariant VGPRs, reloaded once per unit run)
       wgx_cfg<2, 5, 3, 8, 0, 1>("wx25s3k"), wgx_cfg<2, 5, 4, 8, 0, 1>("wx25s4k"), wgx_cfg<2, 5, 6, 8, 0, 1>("wx25s6k"),
       wgx_cfg<2, 5, 6, 4, 0, 1>("wx25s6w4k"), wgx_cfg<2, 5, 8, 4, 0, 1>("wx25s8w4k"), wgx_cfg<2, 5, 12, 4, 0, 1>("wx25s12w4k"),
@@ -852,7 +876,29 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
   uint32_t G = (uint32_t)units;
-  if (c.dc_wpm) {
+  if (c.dc_wpm == 2) {
+    // whole units in full rounds of the resident blocks; the tail round's T units in S pieces each
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)XNT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+    const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+    const uint64_t C = (uint64_t)ncu * (uint32_t)std::min(occ, 2);
+    const uint64_t R = units / C, T = units - R * C;
+    const uint32_t S = T ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(p.ipt, C / T)) : 1u;
+    if (S == 1) {
+      p.ipb = (uint32_t)units;  // nothing to split: every block takes a whole unit
+      p.total_it = 1;
+    } else {
+      p.ipb = (uint32_t)(R * C);
+      p.total_it = S;
+      G = (uint32_t)(R * C + T * S);
+      const size_t slab = (size_t)(16 / (XNT / ((XNT / 64 / NPG) * 64))) * XNT * MO * MO;
+      int rc = ensure_ws(ctx, (size_t)2 * G * slab * 4);
+      if (rc == BH_OK) rc = ensure_cnt(ctx, units);
+      if (rc != BH_OK) return rc;
+      p.ws = (float *)ctx->ws;
+      p.cnt = (uint32_t *)ctx->cnt;
+    }
+  } else if (c.dc_wpm) {
     // stream-K: as many blocks as are resident at once, the (unit, stage) iterations dealt equally
     
     int occ = 0;

@@ -156,3 +156,22 @@ def test_wx_dword_aligned_pointers(dev, cn):
     np.testing.assert_array_equal(got, ref)
     for x in (bi, bo, f, b):
         x.free()
+
+
+# A shape whose unit count leaves a partly filled last round on 256 CUs, so the split-tail grids (wx*t)
+# cut its units into pieces: 640 F(2x2, 5x5) units of 64 channels, 8-wave blocks (one per CU)
+TAIL = {
+    "wx25": C(4, 16, 64, 64, 320, 5, 5, 1, 1, 2, 2),
+}
+
+
+@pytest.mark.parametrize("cn", [n for n in WX if n.endswith("t")])
+def test_wx_split_tail(dev, cn):
+    s = TAIL[cn[:4]]
+    dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
+    try:
+        out = run_conv(dev, s)
+        check(out, s)
+        np.testing.assert_array_equal(run_conv(dev, s), out)  # the tail pieces sum in block order
+    finally:
+        dev.tune_set(1, -1, 0)
