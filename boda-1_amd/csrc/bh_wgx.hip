@@ -147,7 +147,9 @@ __device__ __forceinline__ uint32_t wx_lb(uint32_t bid, uint32_t G) {
 // iterations equally between the blocks; a unit cut between blocks is summed after the output
 // transform (linear) by its last-arriving block in block order (bitwise reproducible)
 // SK = 2: whole units in full rounds of resident blocks, the last partial round's units split into S
-// pieces along the stages (the same slab hand-off), so the tail runs S times shorter
+// pieces along the stages (the same slab hand-off), so the tail runs S times shorter; SK = 3: the
+// tail units split by channel group instead (NOG pieces, each a whole unit's stages for 32 output
+// channels: no partial sums, one MFMA-issuing wave per SIMD)
 template <int MO, int R, int SP, int NW, int SK, int DBG = 0>
 __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   using G = wx_geom<MO, R, NW>;
@@ -170,7 +172,11 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   // (SK 2: the hardware's dispatch order itself -- the whole units go out first, spread over all
   // XCDs, and the tail pieces fill the CUs as they free; the XCD-contiguous remap would hand some XCDs
   // only whole units and others only pieces)
-  const uint32_t lb = SK == 2 ? blockIdx.x : wx_lb(blockIdx.x, gridDim.x);
+  const uint32_t lb = SK >= 2 ? blockIdx.x : wx_lb(blockIdx.x, gridDim.x);
+  // SK 3: a tail piece computes only channel group `piece` of its unit (the other waves transform,
+  // load and synchronise as usual but issue no MFMA and no U load, and store nothing)
+  const int piece = (SK == 3 && lb >= p.ipb) ? (int)((lb - p.ipb) % p.total_it) : -1;
+  const bool active = piece < 0 || og == piece;  // wave-uniform
   const uint32_t ipt = p.ipt;
   // this block's iterations: SK -- [lb * ipb, + ipb); else unit lb. OC tile slowest in the unit order:
   // an XCD's run of units shares few OC tiles' U slices
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   };
   float ur[2][PPG];
   auto load_u = [&](int s, uint32_t it) {
-    const uint32_t su = it < sb ? it * (uint32_t)XC * p.OC32 * (uint32_t)(P * 4) : 0x7fffff00u;  // dead: misses
+    const uint32_t su = (it < sb && active) ? it * (uint32_t)XC * p.OC32 * (uint32_t)(P * 4) : 0x7fffff00u;  // dead: misses
     const f32x4v a = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][0], su, 0));
     const f32x4v b = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[s][1], su, 0));
 #pragma unroll
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
                      uint32_t ox0) {
     const uint32_t ee = (uint32_t)(r * ECH) + rel;
     const uint32_t oc = oc0 + rog * 32u + 8u * (ee >> 2) + 4u * (rlane >> 5) + (ee & 3u);
-    const bool ok = tvalid & (oc < p.OC);
+    const bool ok = tvalid & (oc < p.OC) & (piece < 0 || rog == (uint32_t)piece);
     const uint32_t ob = obase + oc * p.OHW;
 #pragma unroll
     for (int yy = 0; yy < MO; ++yy) {
@@ -473,7 +479,9 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       vm_wait<NLU + SP>();
 #pragma unroll
       for (int q = 0; q < PPG; ++q) {
-        if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+        if constexpr ((DBG & 2) == 0) {
+          if (SK != 3 || active) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[0][q], vf[0][q], acc[q], 0, 0, 0);
+        }
         else asm volatile("" ::"v"(ur[0][q]), "v"(vf[0][q]));
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -487,7 +495,9 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       vm_wait<SP + NLU>();
 #pragma unroll
       for (int q = 0; q < PPG; ++q) {
-        if constexpr ((DBG & 2) == 0) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+        if constexpr ((DBG & 2) == 0) {
+          if (SK != 3 || active) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[1][q], vf[1][q], acc[q], 0, 0, 0);
+        }
         else asm volatile("" ::"v"(ur[1][q]), "v"(vf[1][q]));
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -651,7 +661,11 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       }
     }
   };
-  if constexpr (SK == 2) {
+  if constexpr (SK == 3) {
+    // whole units in full rounds; a tail unit as total_it (= NOG) pieces, one channel group each
+    sb = ipt;
+    run(lb < p.ipb ? lb : p.ipb + (lb - p.ipb) / p.total_it, 0u, true);
+  } else if constexpr (SK == 2) {
     // data-parallel rounds + a split tail: blocks below ipb take their unit whole; the rest take
     // part j of S = total_it of a tail unit (stages [j ipt / S, (j + 1) ipt / S)), so the last,
     // partly filled round of units runs as S times as many shorter pieces
@@ -685,7 +699,7 @@ cfg_t wgx_cfg(const char *name) {
   using G = wx_geom<MO, R, NW>;
   cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
   c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, SK, DBG>;
-  c.dc_wpm = SK;  // (dc == 5) 1: persistent stream-K grid, 2: whole units + a split tail
+  c.dc_wpm = SK;  // (dc == 5) 1: persistent stream-K grid, 2 / 3: whole units + a split tail
   c.dc = 5;
   c.dc_ky = R;
   c.dc_kx = R;
@@ -776,6 +790,9 @@ std::vector<cfg_t> wgx_cfgs() {
       // last arriver reads a whole 16-float-per-pair partial output through the write-through slab),
       // F(2x2, 3x3) no gain: those forms are not built
       wgx_cfg<2, 5, 4, 8, 0, 2>("wx25s4t"), wgx_cfg<2, 5, 6, 8, 0, 2>("wx25s6t"),
+      // whole units + a tail split by channel group (SK 3)
+      wgx_cfg<4, 3, 10, 8, 0, 3>("wx43s10g"), wgx_cfg<4, 3, 12, 8, 0, 3>("wx43s12g"),
+      wgx_cfg<2, 5, 4, 8, 0, 3>("wx25s4g"), wgx_cfg<2, 5, 6, 8, 0, 3>("wx25s6g"),
       // (the F(2x2, 5x5) forms spill ~20 loop-invariant VGPRs, reloaded once per unit run)
       wgx_cfg<2, 5, 3, 8, 0, 1>("wx25s3k"), wgx_cfg<2, 5, 4, 8, 0, 1>("wx25s4k"), wgx_cfg<2, 5, 6, 8, 0, 1>("wx25s6k"),
       wgx_cfg<2, 5, 6, 4, 0, 1>("wx25s6w4k"), wgx_cfg<2, 5, 8, 4, 0, 1>("wx25s8w4k"), wgx_cfg<2, 5, 12, 4, 0, 1>("wx25s12w4k"),
@@ -876,7 +893,23 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
   uint32_t G = (uint32_t)units;
-  if (c.dc_wpm == 2) {
+  if (c.dc_wpm == 3) {
+    // whole units in full rounds of the resident blocks; the tail round's T units as NOG pieces each,
+    // when they fit one round
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)XNT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+    const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+    const uint64_t C = (uint64_t)ncu * (uint32_t)std::min(occ, 2);
+    const uint32_t NOG = XNT / 64 / NPG;
+    const uint64_t R = units / C, T = units - R * C;
+    p.ipb = (uint32_t)units;
+    p.total_it = 1;
+    if (T && NOG > 1 && T * NOG <= C) {
+      p.ipb = (uint32_t)(R * C);
+      p.total_it = NOG;
+      G = (uint32_t)(R * C + T * NOG);
+    }
+  } else if (c.dc_wpm == 2) {
     // whole units in full rounds of the resident blocks; the tail round's T units in S pieces each
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)XNT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;

@@ -158,14 +158,16 @@ def test_wx_dword_aligned_pointers(dev, cn):
         x.free()
 
 
-# A shape whose unit count leaves a partly filled last round on 256 CUs, so the split-tail grids (wx*t)
-# cut its units into pieces: 640 F(2x2, 5x5) units of 64 channels, 8-wave blocks (one per CU)
+# Shapes whose unit count leaves a partly filled last round on 256 CUs, so the split-tail grids cut
+# its units into pieces (wx*t: along the stages, wx*g: by channel group): 288 F(4x4, 3x3) and 640
+# F(2x2, 5x5) units of 64 channels, 8-wave blocks (one per CU)
 TAIL = {
+    "wx43": C(9, 8, 128, 128, 64, 3, 3, 1, 1, 1, 1),
     "wx25": C(4, 16, 64, 64, 320, 5, 5, 1, 1, 2, 2),
 }
 
 
-@pytest.mark.parametrize("cn", [n for n in WX if n.endswith("t")])
+@pytest.mark.parametrize("cn", [n for n in WX if n.endswith(("t", "g"))])
 def test_wx_split_tail(dev, cn):
     s = TAIL[cn[:4]]
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
