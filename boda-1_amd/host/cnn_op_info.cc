@@ -152,7 +152,7 @@ struct latex_rows_t {
 
 // comp_vars for one var pair (src/comp_util.cc:21-57 with ssds_diff_t, src/boda_base.cc:126-207)
 bool comp_var(std::ostream &out, std::string const &vn, dims_t const &dims, std::vector<float> const &o1,
-              std::vector<float> const &o2, double toler, uint32_t max_err) {
+              std::vector<float> const &o2, double toler, uint32_t max_err, double *mrd_out) {
   double ssds = 0, sds = 0, mad = 0, mrd = 0, s1 = 0, s2 = 0;
   uint64_t ndiff = 0;
   const size_t n = o1.size();
@@ -167,6 +167,7 @@ bool comp_var(std::ostream &out, std::string const &vn, dims_t const &dims, std:
     ndiff += o1[i] != o2[i];
   }
   const bool nan = std::isnan(ssds) || std::isnan(sds) || std::isnan(mad);
+  *mrd_out = nan ? NAN : mrd;
   if (!(mrd >= toler || nan)) return false;
   out << vn << ": DIMS[" << dims.str() << "] ssds_str(out_batch_1,out_batch_2)=cnt=" << ndiff
       << " sum_squared_diffs=" << raw_str(ssds) << " avg_abs_diff=" << raw_str(std::sqrt(ssds / n))
@@ -223,7 +224,8 @@ int main(int argc, char **argv) {
     std::cerr << "usage: boda_hip_cnn_op_info --cnn-func-sigs-fn=F [--out-fn=F] [--op-info-tab-fn=F]\n"
                  "  [--op-eff-tab-fn=F] [--print-format=0|1|2] [--inc-op-info-in-eff=0] [--peak-flops=157.3e12]\n"
                  "  [--run-iter=1] [--graph-reps=0] [--gen-data-mode=5] [--comp=vendor|none] [--mrd-toler=2e-4]\n"
-                 "  [--max-err=10] [--device=0] [--eff-comp=1] [--no-run=1] | --pp-vals=v,v,...\n";
+                 "  [--max-err=10] [--wino-mrd-toler=2e-2] [--show-mrd=1] [--device=0]\n"
+                 "  [--eff-comp=1] [--no-run=1] | --pp-vals=v,v,...\n";
     return 2;
   }
   try {
@@ -244,6 +246,12 @@ int main(int argc, char **argv) {
     const uint32_t graph_reps = std::stoul(o.get("graph-reps", "0"));
     const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
     const double toler = std::stod(o.get("mrd-toler", "2e-4"));
+    // Winograd routes (variant names *_wino_*) compare at their own tolerance, as ops-prof widens its
+    // compare for cuDNN's Winograd (src/rtc_prof.cc:314-319): the input / output transforms turn
+    // cancellation in the direct sum into element errors min_sig_mag_rel_diff sees on near-zero
+    // outputs (measured per op with --show-mrd=1)
+    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-2"));
+    const bool show_mrd = o.get("show-mrd", "0") != "0";
     const uint32_t max_err = std::stoul(o.get("max-err", "10"));
     const std::string comp = o.get("comp", "vendor");
     if (comp != "vendor" && comp != "none") rt_err("--comp must be vendor or none");
@@ -315,6 +323,20 @@ int main(int argc, char **argv) {
       if (graph_reps) secs = rtc->time_graph([&] { rtc->run(c); }, graph_reps) / 1e3;
       p_nda_t o1 = rtc->create_nda_from_var(ovn);
 
+      char vb[160] = "";
+      {
+        std::vector<uint32_t> dims;
+        if (conv) {
+          conv_shape_t s = get_conv_shape(op);
+          dims = {s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px};
+        } else {
+          sgemm_shape_t s = get_sgemm_shape(op);
+          dims = {s.M, s.N, s.K};
+        }
+        if (bh_variant_name(conv ? 1 : 0, dims.data(), vb, sizeof vb) != 0)
+          std::snprintf(vb, sizeof vb, "%s", op.func_name.c_str());
+      }
+      const bool wino = std::string(vb).find("_wino_") != std::string::npos;
       double secs_comp = NAN;
       if (vctx) {
         // the comparator on the same device inputs, into a second output var
@@ -339,20 +361,14 @@ int main(int argc, char **argv) {
         secs_comp = ms / 1e3;
         p_nda_t o2 = rtc->create_nda_from_var("comp_" + ovn);
         *out << "vars_to_compare: " << ovn << "\n";
-        if (comp_var(*out, ovn, o1->dims, *o1->data, *o2->data, toler, max_err)) ++num_mad_fail;
+        double mrd = 0;
+        if (comp_var(*out, ovn, o1->dims, *o1->data, *o2->data, wino ? wino_toler : toler, max_err, &mrd))
+          ++num_mad_fail;
+        if (show_mrd) *out << ovn << ": max_rel_diff=" << raw_str(mrd) << " toler=" << (wino ? wino_toler : toler)
+                           << " variant=" << vb << "\n";
         rtc->release_var("comp_" + ovn);
       }
       if (oet.is_open()) {
-        char vb[160] = "";
-        std::vector<uint32_t> dims;
-        if (conv) {
-          conv_shape_t s = get_conv_shape(op);
-          dims = {s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px};
-        } else {
-          sgemm_shape_t s = get_sgemm_shape(op);
-          dims = {s.M, s.N, s.K};
-        }
-        if (bh_variant_name(conv ? 1 : 0, dims.data(), vb, sizeof vb) != 0) std::snprintf(vb, sizeof vb, "%s", op.func_name.c_str());
         oet << lx.eff_row(vb, secs, peak, secs_comp);
         oet.flush();
       }

@@ -15,8 +15,11 @@ modes 600 / 5 on sgemm-ops-debug / conv-ops-debug) print "vars_to_compare: c|out
 for both sides. Tolerance: the reference loosens its own vendor comparison (ops-prof
 --func-mrd-toler='(cudnn_conv=4e-4)', test/test_cmds.xml:110). Ours against rocBLAS / MIOpen
 measured max min_sig_mag_rel_diff up to 7.2e-4 (SGEMM 2048^3, mode 5; 1.1e-3 at 1536^3) and 4.3e-4
-(conv), two fp32 accumulation orders apart, so the comparator runs here at 2e-3 (SGEMM) / 1e-3
-(conv); our own kernels are held to the float64 oracle elsewhere (test_gpu_sgemm / test_gpu_conv).
+(direct / GEMM conv routes), two fp32 accumulation orders apart, so the comparator runs here at
+2e-3 (SGEMM) / 1e-3 (conv). Winograd routes compare at the driver's --wino-mrd-toler (2e-2; up to
+8.8e-3 measured on near-zero outputs of the 5x5 / F(4x4,3x3) routes), as ops-prof widens its own
+compare for cuDNN's Winograd (src/rtc_prof.cc:314-319). Our kernels are held to the float64 oracle
+at the suite's normalized tolerances elsewhere (test_gpu_sgemm / test_gpu_conv / test_gpu_wgx).
 """
 import math
 import os
@@ -81,13 +84,15 @@ def test_cnn_op_info_all_is_well_vs_vendor(fn, mode, var, tmp_path):
     assert os.path.exists(BIN), "boda_hip_cnn_op_info not built"
     eff = tmp_path / "eff.tex"
     r = subprocess.run([BIN, "--cnn-func-sigs-fn=" + os.path.join(OPS, fn), "--gen-data-mode=%d" % mode,
-                        "--op-eff-tab-fn=" + str(eff), "--max-err=10", "--mrd-toler=" + toler],
+                        "--op-eff-tab-fn=" + str(eff), "--max-err=10", "--mrd-toler=" + toler, "--show-mrd=1"],
                        capture_output=True, text=True, timeout=110)
     print(r.stdout[-3000:], r.stderr[-2000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr
     assert r.stdout.strip().endswith("***ALL IS WELL***")
     n = len(ops.read_ops(os.path.join(OPS, fn))[0])
     assert r.stdout.count("vars_to_compare: %s\n" % var) == n
+    mrds = re.findall(r"max_rel_diff=(\S+) toler=(\S+) variant=(\S+)", r.stdout)
+    assert len(mrds) == n and all(float(m) < float(t) for m, t, _ in mrds), mrds
     rows = open(eff).read().splitlines()
     assert len(rows) == n
     for row in rows:

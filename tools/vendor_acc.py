@@ -50,7 +50,9 @@ def conv64(x, f, b, s):  # float64 conv + bias + ReLU, NCHW
 
 
 for dims in [(5, 64, 14, 14, 64, 3, 3, 1, 1, 1, 1), (20, 3, 227, 227, 96, 11, 11, 4, 4, 0, 0),
-             (5, 96, 27, 27, 256, 5, 5, 1, 1, 2, 2)]:
+             (5, 96, 27, 27, 256, 5, 5, 1, 1, 2, 2), (20, 96, 27, 27, 256, 5, 5, 1, 1, 2, 2),
+             (20, 64, 56, 56, 192, 3, 3, 1, 1, 1, 1), (20, 32, 28, 28, 96, 5, 5, 1, 1, 2, 2),
+             (20, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)]:
     s = ops.ConvShape(*dims)
     i, f, b = dev.alloc_floats(s.B * s.IC * s.H * s.W), dev.alloc_floats(s.OC * s.IC * s.KY * s.KX), \
         dev.alloc_floats(s.OC)
@@ -65,8 +67,10 @@ for dims in [(5, 64, 14, 14, 64, 3, 3, 1, 1, 1, 1), (20, 3, 227, 227, 96, 11, 11
     ref = conv64(i.download().reshape(s.B, s.IC, s.H, s.W).astype(np.float64),
                  f.download().reshape(s.OC, s.IC, s.KY, s.KX).astype(np.float64), b.download().astype(np.float64), s)
     o, v = o1.download().reshape(ref.shape), o2.download().reshape(ref.shape)
-    print("conv %s: ours %.3g  vendor %.3g  ours-vs-vendor %.3g" % (list(dims), msr(ref, o), msr(ref, v),
-                                                                  msr(o.astype(np.float64), v)), flush=True)
+    nm = lambda x: float(np.max(np.abs(x - ref)) / np.max(np.abs(ref)))  # noqa: E731  (the tests' normalized max)
+    print("conv %s [%s]: ours %.3g (norm-max %.2g)  vendor %.3g (norm-max %.2g)  ours-vs-vendor %.3g"
+          % (list(dims), boda_hip.variant_name(1, s.as_dims()), msr(ref, o), nm(o),
+             msr(ref, v), nm(v), msr(o.astype(np.float64), v)), flush=True)
     for x in (i, f, b, o1, o2):
         x.free()
 vd.close()
