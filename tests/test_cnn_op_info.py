@@ -14,11 +14,14 @@ modes 600 / 5 on sgemm-ops-debug / conv-ops-debug) print "vars_to_compare: c|out
 ***ALL IS WELL*** (good_tr/test_cnn_op_info_*/cnn_op_info.txt); the eff rows carry finite runtimes
 for both sides. Tolerance: the reference loosens its own vendor comparison (ops-prof
 --func-mrd-toler='(cudnn_conv=4e-4)', test/test_cmds.xml:110). Ours against rocBLAS / MIOpen
-measured max min_sig_mag_rel_diff up to 7.2e-4 (SGEMM 2048^3, mode 5; 1.1e-3 at 1536^3) and 4.3e-4
-(direct / GEMM conv routes), two fp32 accumulation orders apart, so the comparator runs here at
-2e-3 (SGEMM) / 1e-3 (conv). Winograd routes compare at the driver's --wino-mrd-toler (2e-2; up to
-8.8e-3 measured on near-zero outputs of the 5x5 / F(4x4,3x3) routes), as ops-prof widens its own
-compare for cuDNN's Winograd (src/rtc_prof.cc:314-319). Our kernels are held to the float64 oracle
+measured max min_sig_mag_rel_diff up to 7.2e-4 (SGEMM 2048^3, mode 5; 1.1e-3 at 1536^3) and 1.56e-3
+(direct / GEMM conv routes over the 204 conv-set ops; MIOpen itself is 1.17e-3 from float64 on
+20x384x13^2->384): two fp32 accumulation orders apart, with cancellation on near-zero outputs that
+min_sig_mag_rel_diff measures absolutely. The comparator runs here at 2e-3 (SGEMM) / 3e-3 (conv);
+Winograd routes at the driver's --wino-mrd-toler (2e-2; up to 8.8e-3 measured, 5x5 / F(4x4,3x3)),
+as ops-prof widens its own compare for cuDNN's Winograd (src/rtc_prof.cc:314-319). Normalized
+(max|d| / max|ref|) the same outputs are within 8.6e-6 of float64 (tools/vendor_acc.py,
+profiles/r04/cnn_op_info/vendor_acc.txt). Our kernels are held to the float64 oracle
 at the suite's normalized tolerances elsewhere (test_gpu_sgemm / test_gpu_conv / test_gpu_wgx).
 """
 import math
@@ -80,7 +83,7 @@ def test_raw_eff_rows_parse_as_op_eff_plot(fn, tmp_path):
 @pytest.mark.parametrize("fn,mode,var", [("sgemm-ops-debug.txt", 600, "c"), ("sgemm-ops-debug.txt", 5, "c"),
                                          ("conv-ops-debug.txt", 5, "out"), ("conv-ops-small.txt", 5, "out")])
 def test_cnn_op_info_all_is_well_vs_vendor(fn, mode, var, tmp_path):
-    toler = "2e-3" if var == "c" else "1e-3"
+    toler = "2e-3" if var == "c" else "3e-3"
     assert os.path.exists(BIN), "boda_hip_cnn_op_info not built"
     eff = tmp_path / "eff.tex"
     r = subprocess.run([BIN, "--cnn-func-sigs-fn=" + os.path.join(OPS, fn), "--gen-data-mode=%d" % mode,

@@ -8,7 +8,7 @@ tools/gpu_job.sh \
   coitests 300 python -u -m pytest tests/test_cnn_op_info.py -x -v --timeout 120 --timeout-method thread :: \
   coiconv 600 $B --cnn-func-sigs-fn=tests/golden/ops/conv-ops-1-5-20-nin-alex-gn.txt --run-iter=5 --graph-reps=40 \
     --out-fn=gpurun_out/cnn_op_info_conv.txt --op-info-tab-fn=gpurun_out/conv_info_tab.tex \
-    --op-eff-tab-fn=gpurun_out/conv_eff_tab.tex --eff-comp=1 --mrd-toler=1e-3 --show-mrd=1 :: \
+    --op-eff-tab-fn=gpurun_out/conv_eff_tab.tex --eff-comp=1 --mrd-toler=3e-3 --show-mrd=1 :: \
   coiconvraw 600 $B --cnn-func-sigs-fn=tests/golden/ops/conv-ops-1-5-20-nin-alex-gn.txt --comp=none --run-iter=5 \
     --graph-reps=40 --print-format=1 --inc-op-info-in-eff=1 --op-eff-tab-fn=gpurun_out/conv_eff_tab.raw :: \
   coisgemm 300 $B --cnn-func-sigs-fn=tests/golden/ops/sgemm-ops-small.txt --run-iter=5 --graph-reps=10 \
