@@ -6,8 +6,8 @@
 //     src/latex-util.H:59-68; never brief there, as the reference);
 //   * runs the op on the hand-written MI355X kernels (be=hip, libboda_hip.so) on gen_data inputs,
 //     --run-iter times, and takes the event time of the last call (profile_rcg_call,
-//     src/rtc_prof.cc:44-126); --graph-reps=N instead replays N calls as one hipGraph and takes the
-//     per-call time (the bench's per-op convention);
+//     src/rtc_prof.cc:44-126); --graph-reps=N instead captures N back-to-back calls in one hipGraph,
+//     replays it and takes the per-call time (the bench's per-op convention);
 //   * with --comp=vendor (the default, the reference's use_culibs=1 comparator,
 //     src/cnn-prof.cc:40,90-91 / src/culibs-wrap.cc:94-242), runs the same op through rocBLAS / MIOpen
 //     (libboda_hip_vendor.so) on the SAME device inputs into its own output, prints
@@ -320,7 +320,9 @@ int main(int argc, char **argv) {
       for (uint32_t r = 0; r < run_iter; ++r) call_id = rtc->run(c);
       rtc->finish_and_sync();
       double secs = rtc->get_dur(call_id, call_id) / 1e3;
-      if (graph_reps) secs = rtc->time_graph([&] { rtc->run(c); }, graph_reps) / 1e3;
+      // graph_reps back-to-back calls captured in one graph, replayed 3 times: the per-call time
+      if (graph_reps)
+        secs = rtc->time_graph([&] { for (uint32_t r = 0; r < graph_reps; ++r) rtc->run(c); }, 3) / graph_reps / 1e3;
       p_nda_t o1 = rtc->create_nda_from_var(ovn);
 
       char vb[160] = "";
