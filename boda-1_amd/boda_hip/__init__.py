@@ -23,13 +23,15 @@ GEN_SGEMM_A, GEN_SGEMM_B, GEN_CONV_IN, GEN_CONV_FILTS, GEN_CONV_BIASES = range(5
 EXPORTS = ["bh_abi_version", "bh_last_error", "bh_device_count", "bh_init", "bh_destroy", "bh_plat_tag",
            "bh_get_stream", "bh_alloc", "bh_free", "bh_memset0", "bh_h2d", "bh_d2h", "bh_sync",
            "bh_event_record", "bh_elapsed_ms", "bh_events_reset", "bh_gen_data", "bh_sgemm_kmajor",
-           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_tune_set", "bh_tune_set_policy", "bh_tune_cfg_name",
+           "bh_conv2d_fwd_nchw", "bh_variant_name", "bh_variant_name_ctx", "bh_tune_set", "bh_tune_set_policy", "bh_tune_cfg_name",
            "bh_capture_begin", "bh_capture_end", "bh_graph_launch", "bh_graph_destroy",
            "bh_stamp", "bh_stamps_read", "bh_time_next_call", "bh_spin", "bh_conv2d_fwd_nchw_pk",
            "bh_conv_filts_packed_floats", "bh_conv_filts_pack", "bh_pool_out_size", "bh_pool_fwd_nchw",
            "bh_lrn_fwd_nchw", "bh_relu_inplace", "bh_dropout_inplace", "bh_softmax_chans", "bh_chan_copy", "bh_chan_affine",
            "bh_eltwise", "bh_conv2d_fwd_nchw_slab", "bh_conv2d_fwd_nchw_res", "bh_jit_build", "bh_jit_compile",
-           "bh_jit_launch", "bh_jit_release"]
+           "bh_jit_launch", "bh_jit_release", "bh_conv_filts_packed_floats_banks", "bh_conv_filts_pack_banks",
+           "bh_conv_route_banks", "bh_conv2d_fwd_nchw_pkb"]
+BANK_W23, BANK_W43, BANK_W25, BANKS_ALL = 1, 2, 4, 0xffffffff
 
 
 class BodaHipError(RuntimeError):
@@ -79,6 +81,11 @@ def lib():
         L.bh_conv_filts_packed_floats.argtypes = [c_u32] * 4
         L.bh_conv_filts_packed_floats.restype = ctypes.c_size_t
         L.bh_conv_filts_pack.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 4
+        L.bh_conv_filts_packed_floats_banks.argtypes = [c_u32] * 5
+        L.bh_conv_filts_packed_floats_banks.restype = ctypes.c_size_t
+        L.bh_conv_filts_pack_banks.argtypes = [c_vp, c_vp, c_vp] + [c_u32] * 5
+        L.bh_conv_route_banks.argtypes = [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]
+        L.bh_conv2d_fwd_nchw_pkb.argtypes = [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_vp] + [c_u32] * 13 + [ctypes.c_int]
         L.bh_pool_out_size.argtypes = [c_u32] * 4
         L.bh_pool_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 10 + [ctypes.c_int]
         L.bh_lrn_fwd_nchw.argtypes = [c_vp, c_vp, c_vp, c_vp] + [c_u32] * 5 + [ctypes.c_float] * 3
@@ -89,6 +96,7 @@ def lib():
         L.bh_chan_affine.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp] + [c_u32] * 3 + [ctypes.c_int]
         L.bh_eltwise.argtypes = [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.bh_variant_name.argtypes = [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
+        L.bh_variant_name_ctx.argtypes = [c_vp, ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_char_p, ctypes.c_size_t]
         L.bh_stamp.argtypes = [c_vp, ctypes.c_int]
         L.bh_spin.argtypes = [c_vp, ctypes.c_int]
         L.bh_time_next_call.argtypes = [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -125,9 +133,12 @@ def variant_name(op_kind, dims):
     return buf.value.decode()
 
 
-def conv_filts_packed_floats(s):
-    """Floats of the transformed filter bank (bh_conv_filts_pack) for conv shape s."""
-    return lib().bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX)
+def conv_filts_packed_floats(s, banks=None):
+    """Floats of the transformed filter bank for conv shape s: the full pack (bh_conv_filts_pack), or
+    with banks (a BANK_* mask) the k-major bank + those Winograd banks (bh_conv_filts_pack_banks)."""
+    if banks is None:
+        return lib().bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX)
+    return lib().bh_conv_filts_packed_floats_banks(s.OC, s.IC, s.KY, s.KX, banks)
 
 
 def pool_out_size(n, k, stride, pad):
@@ -278,6 +289,13 @@ class Device:
     def tune_set(self, op_kind, cfg_index=-1, splits=0):
         _check(lib().bh_tune_set(self.ctx, op_kind, cfg_index, splits))
 
+    def variant(self, op_kind, dims):
+        """The kernel variant a call on this context runs now (with its tune overrides)."""
+        arr = (c_u32 * 16)(*dims)
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().bh_variant_name_ctx(self.ctx, op_kind, arr, buf, 256))
+        return buf.value.decode()
+
     def tune_set_policy(self, op_kind, wt=-1):
         """Output store policy override: 1 write-through, 0 write-back, -1 the table's choice."""
         _check(lib().bh_tune_set_policy(self.ctx, op_kind, wt))
@@ -336,6 +354,26 @@ class Device:
     def eltwise(self, a, b, out, n, op=1, relu=0):
         _check(lib().bh_eltwise(self.ctx, a.ptr, b.ptr, out.ptr, n, op, int(relu)))
 
-    def conv_filts_pack(self, filts, packed, s):
-        """Boda's xpose_filts counterpart: write the k-major bank of filts into packed."""
-        _check(lib().bh_conv_filts_pack(self.ctx, filts.ptr, packed.ptr, s.OC, s.IC, s.KY, s.KX))
+    def conv_filts_pack(self, filts, packed, s, banks=None):
+        """Boda's xpose_filts counterpart: write the k-major bank of filts (+ the Winograd banks: all of
+        the kernel size's, or those of the mask banks) into packed."""
+        if banks is None:
+            _check(lib().bh_conv_filts_pack(self.ctx, filts.ptr, packed.ptr, s.OC, s.IC, s.KY, s.KX))
+        else:
+            _check(lib().bh_conv_filts_pack_banks(self.ctx, filts.ptr, packed.ptr, s.OC, s.IC, s.KY, s.KX, banks))
+
+    def route_banks(self, s):
+        """The Winograd bank mask the route of conv shape s on this context reads (0: k-major only)."""
+        arr = (c_u32 * 11)(*s.as_dims())
+        b = c_u32(0)
+        _check(lib().bh_conv_route_banks(self.ctx, arr, ctypes.byref(b)))
+        return b.value
+
+    def conv_pkb(self, inp, filts, packed, banks, biases, out, s, relu=1, res=None, out_chans_total=0,
+                 out_chan_ofs=0):
+        """bh_conv2d_fwd_nchw_pkb: packed (may be None) holds the k-major bank + the banks of mask banks."""
+        _check(lib().bh_conv2d_fwd_nchw_pkb(self.ctx, inp.ptr, filts.ptr, packed.ptr if packed is not None else None,
+                                            banks, biases.ptr if biases is not None else None,
+                                            res.ptr if res is not None else None, out.ptr, out_chans_total,
+                                            out_chan_ofs, s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py,
+                                            s.px, int(relu)))

@@ -124,10 +124,14 @@ int tune_set_wt(bh_ctx *ctx, int op, int wt);
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases,
                 float *out, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                 uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot = 0,
-                const float *res = nullptr, bool no_dc = false, bool repacked = false);
-size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
+                const float *res = nullptr, bool no_dc = false, bool repacked = false,
+                uint32_t pk_banks = 0xffffffffu);
+// packs (bhk::launch_pack_banks): the k-major bank + the Winograd banks of `banks` (BH_BANK_*)
+size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks);
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
-                           uint32_t KX);
+                           uint32_t KX, uint32_t banks);
+// the Winograd bank (BH_BANK_*, 0: none) the shape's route on ctx reads
+uint32_t conv_route_banks(bh_ctx *ctx, const uint32_t *d);
 uint32_t pool_out_sz(uint32_t in, uint32_t k, uint32_t s, uint32_t p);
 int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint32_t B, uint32_t C, uint32_t H,
                 uint32_t W, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int avg);
@@ -143,6 +147,8 @@ int launch_chan_affine(bh_ctx *ctx, const float *in, float *out, const float *sc
 int launch_eltwise(bh_ctx *ctx, const float *a, const float *b, float *out, uint64_t n, int op, int relu);
 std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K);
 std::string conv_variant(const uint32_t *d);
+std::string sgemm_variant_ctx(bh_ctx *ctx, uint32_t M, uint32_t N, uint32_t K);  // with ctx's overrides
+std::string conv_variant_ctx(bh_ctx *ctx, const uint32_t *d);
 int tune_set(bh_ctx *ctx, int op, int cfg, int splits);
 int tune_cfg_name(int op, int cfg, std::string &out);
 void jit_release_all(bh_ctx *c);

@@ -1106,6 +1106,18 @@ std::string sgemm_variant(uint32_t M, uint32_t N, uint32_t K) {
 
 std::string conv_variant(const uint32_t *d) { return describe(1, d, choose(nullptr, 1, d)); }
 
+uint32_t conv_route_banks(bh_ctx *ctx, const uint32_t *d) {
+  choice_t ch = choose(ctx, 1, d);
+  return cfgs(1)[ch.cfg].packA ? bhk::route_bank(cfgs(1)[ch.cfg], d[5], d[6]) : 0u;
+}
+
+std::string sgemm_variant_ctx(bh_ctx *ctx, uint32_t M, uint32_t N, uint32_t K) {
+  uint32_t d[3] = {M, N, K};
+  return describe(0, d, choose(ctx, 0, d));
+}
+
+std::string conv_variant_ctx(bh_ctx *ctx, const uint32_t *d) { return describe(1, d, choose(ctx, 1, d)); }
+
 int tune_set(bh_ctx *ctx, int op, int cfg, int splits) {
   if (op < 0 || op > 1) return fail(BH_ERR, "tune_set: op must be 0 (sgemm) or 1 (conv)");
   if (cfg >= (int)cfgs(op).size()) return fail(BH_UNSUP, "tune_set: no such config");
@@ -1153,7 +1165,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
 int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *packed, const float *biases, float *out, uint32_t B,
                 uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy,
                 uint32_t sx, uint32_t py, uint32_t px, int relu, uint32_t out_ctot, const float *res,
-                bool no_dc, bool repacked) {
+                bool no_dc, bool repacked, uint32_t pk_banks) {
   // repacked: a fallback call after this call's filter repack was already dispatched (that repack
   // recorded the call's start event; no kernel of the fallback may record it again)
   // out_ctot: channels of the tensor `out` points into (0: OC). Every conv epilogue addresses
@@ -1235,22 +1247,24 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   }
   if (cfgs(1)[ch.cfg].packA) {
     // ring kernels read the filter bank k-major: repack it first (this call's first dispatch)
-    // (K order (ky, kx, ic), rows padded to a multiple of 64; input offsets + 2^30 must miss)
-    // pk_floats (the whole pack: k-major bank + the Winograd U bank of a 3x3) sizes the buffer and
-    // the 2 GiB check; the k-major kernels see only the k-major part, so reads past it are misses
-    const size_t pk_floats = conv_filts_packed_floats(OC, IC, KY, KX);
+    // (K order (ky, kx, ic), rows padded to a multiple of 64; input offsets + 2^30 must miss).
+    // A Winograd route reads its bank behind it: from the caller's pack when that holds the bank
+    // (pk_banks), otherwise from a pack of just the k-major bank + that bank made here. The 2 GiB
+    // check and the context's pack buffer are sized by what the route reads.
+    const uint32_t need = route_bank(cfgs(1)[ch.cfg], KY, KX);
+    pk_banks &= all_banks(KY, KX);
     const uint32_t oc4 = (OC + 3) & ~3u, kp = (uint32_t)(kmajor_floats(OC, IC, KY, KX) / oc4);
     const float *wp = packed;
-    if (pk_floats * 4 >= 0x7fffffc0ull || in_bytes >= (1ull << 30)) {
+    uint32_t banks = pk_banks;
+    if (wp && need && !(pk_banks & need)) wp = nullptr;  // the caller's pack lacks the route's bank
+    if (!wp) banks = need;
+    if (banks_floats(OC, IC, KY, KX, need) * 4 >= 0x7fffffc0ull || in_bytes >= (1ull << 30)) {
       ch = heuristic(1, d, false);
     } else {
       bool rp = repacked;  // a repack of this call already dispatched (it recorded the start event)
-      const bool wino = cfgs(1)[ch.cfg].dc == 4 || cfgs(1)[ch.cfg].dc == 5;  // reads a Winograd part of the pack
       if (!wp) {
-        int rc = ensure_wpack(ctx, pk_floats * 4);
-        if (rc == BH_OK)
-          rc = wino ? launch_pack_all(ctx, filts, (float *)ctx->wpack, OC, IC, KY, KX, first, false)
-                    : launch_xpose_filts(ctx, filts, (float *)ctx->wpack, OC, IC, KY * KX, first, false);
+        int rc = ensure_wpack(ctx, banks_floats(OC, IC, KY, KX, banks) * 4);
+        if (rc == BH_OK) rc = launch_pack_banks(ctx, filts, (float *)ctx->wpack, OC, IC, KY, KX, banks, first, false);
         if (rc != BH_OK) return rc;
         wp = (const float *)ctx->wpack;
         rp = true;
@@ -1265,20 +1279,20 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
         const cfg_t &dcc = cfgs(1)[ch.cfg];
         const int rc = dcc.dc == 2   ? launch_dcm(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, kfirst)
                        : dcc.dc == 3 ? launch_k1s(ctx, dcc, p, B, KY, KX, sy, sx, ch.splits, kfirst)
-                       : dcc.dc == 4 ? (KY == 3 && KX == 3
-                                            ? launch_wg(ctx, dcc, wp + kmajor_floats(OC, IC, KY, KX), in, biases, res, out,
-                                                        out_ctot, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, p.wt,
+                       : dcc.dc == 4 ? (need
+                                            ? launch_wg(ctx, dcc, wp + bank_offset(OC, IC, KY, KX, banks, need), in, biases, res,
+                                                        out, out_ctot, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, p.wt,
                                                         ch.splits, kfirst)
                                             : bh::fail(BH_UNSUP, std::string("conv: ") + dcc.name + " is for 3x3 convs"))
-                       : dcc.dc == 5 ? (wino_bank_offset(OC, IC, KY, KX, (uint32_t)dcc.dc_s) && KY == (uint32_t)dcc.dc_ky
-                                            ? launch_wgx(ctx, dcc, wp + wino_bank_offset(OC, IC, KY, KX, (uint32_t)dcc.dc_s),
-                                                         in, biases, res, out, out_ctot, B, IC, H, W, OC, KY, KX, sy, sx,
-                                                         py, px, relu, p.wt, ch.splits, kfirst)
+                       : dcc.dc == 5 ? (need
+                                            ? launch_wgx(ctx, dcc, wp + bank_offset(OC, IC, KY, KX, banks, need), in, biases,
+                                                         res, out, out_ctot, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu,
+                                                         p.wt, ch.splits, kfirst)
                                             : bh::fail(BH_UNSUP, std::string("conv: ") + dcc.name + " is for other kernel sizes"))
                                      : launch_dc(ctx, dcc, p, B, KY, KX, sy, sx, kfirst);
         if (rc != BH_UNSUP || (ctx && ctx->ovr_cfg[1] >= 0)) return rc;
         return launch_conv(ctx, in, filts, wp, biases, out, B, IC, H, W, OC, KY, KX, sy, sx, py, px, relu, out_ctot,
-                           res, true, rp);
+                           res, true, rp, banks);
       }
       if (cfgs(1)[ch.cfg].gv) {
         // register streaming over the packed bank (bh_gv.hip gvp_kernel): 16-deep k groups

@@ -398,12 +398,19 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
 size_t wx_bank_floats(uint32_t OC, uint32_t IC);
 int launch_wx_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, uint32_t R, bool first,
                    bool last);
-// every part of a conv pack after the k-major bank: 3x3 -- the F(2x2,3x3) bank, then the F(4x4,3x3)
-// bank; 5x5 -- the F(2x2,5x5) bank. Offsets in floats from the pack's start (0: no such bank)
-size_t pack_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
-size_t wino_bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t MO);
-int launch_pack_all(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX,
-                    bool first, bool last);
+// A conv pack: the k-major bank, then the Winograd banks of its mask in bit order -- F(2x2,3x3)
+// (BANK_W23, bh_wino.hip's [IC4][OC32][16]), F(4x4,3x3) (BANK_W43) and F(2x2,5x5) (BANK_W25, both
+// wx_pack's [IC4][OC32][36]). A mask is cut to the banks of the kernel size (all_banks): the full
+// pack of bh_conv_filts_pack is a 3x3's W23 + W43, a 5x5's W25.
+constexpr uint32_t BANK_W23 = 1u, BANK_W43 = 2u, BANK_W25 = 4u, BANKS_ALL = 0xffffffffu;
+uint32_t all_banks(uint32_t KY, uint32_t KX);
+size_t banks_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks);
+// offset in floats of bank (one BANK_*) in a pack holding banks (it must be one of them)
+size_t bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks, uint32_t bank);
+// the bank a configuration reads (0: the k-major bank only)
+uint32_t route_bank(const cfg_t &c, uint32_t KY, uint32_t KX);
+int launch_pack_banks(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
+                      uint32_t KX, uint32_t banks, bool first, bool last);
 int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint32_t IC, bool first, bool last);
 // floats of the k-major bank (the first part of every pack)
 size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);

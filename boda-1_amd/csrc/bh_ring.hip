@@ -953,30 +953,48 @@ size_t kmajor_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
   return (size_t)(((uint64_t)IC * KY * KX + 63) & ~63ull) * ((OC + 3) & ~3u);
 }
 
-size_t pack_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
-  const size_t km = kmajor_floats(OC, IC, KY, KX);
-  if (KY == 3 && KX == 3) return km + wino_bank_floats(OC, IC) + wx_bank_floats(OC, IC);
-  if (KY == 5 && KX == 5) return km + wx_bank_floats(OC, IC);
-  return km;
-}
-
-size_t wino_bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t MO) {
-  const size_t km = kmajor_floats(OC, IC, KY, KX);
-  if (KY == 3 && KX == 3) return MO == 2 ? km : km + wino_bank_floats(OC, IC);
-  if (KY == 5 && KX == 5 && MO == 2) return km;
+uint32_t all_banks(uint32_t KY, uint32_t KX) {
+  if (KY == 3 && KX == 3) return BANK_W23 | BANK_W43;
+  if (KY == 5 && KX == 5) return BANK_W25;
   return 0;
 }
 
-// the whole pack: k-major bank, then the Winograd banks of the kernel size (a 3x3's F(2x2,3x3) bank
-// (bh_wino.hip) and F(4x4,3x3) bank, a 5x5's F(2x2,5x5) bank (bh_wgx.hip))
-int launch_pack_all(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX,
-                    bool first, bool last) {
-  const bool w3 = KY == 3 && KX == 3, w5 = KY == 5 && KX == 5;
-  const size_t km = kmajor_floats(OC, IC, KY, KX);
-  int rc = launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, first, last && !w3 && !w5);
-  if (rc == BH_OK && w3) rc = launch_wino_pack(ctx, filts, packed + km, OC, IC, false, false);
-  if (rc == BH_OK && w3) rc = launch_wx_pack(ctx, filts, packed + km + wino_bank_floats(OC, IC), OC, IC, 3, false, last);
-  if (rc == BH_OK && w5) rc = launch_wx_pack(ctx, filts, packed + km, OC, IC, 5, false, last);
+static size_t bank_floats(uint32_t bank, uint32_t OC, uint32_t IC) {
+  return bank == BANK_W23 ? wino_bank_floats(OC, IC) : wx_bank_floats(OC, IC);
+}
+
+size_t banks_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks) {
+  banks &= all_banks(KY, KX);
+  size_t n = kmajor_floats(OC, IC, KY, KX);
+  for (uint32_t b = 1; b <= BANK_W25; b <<= 1)
+    if (banks & b) n += bank_floats(b, OC, IC);
+  return n;
+}
+
+size_t bank_offset(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks, uint32_t bank) {
+  return banks_floats(OC, IC, KY, KX, banks & (bank - 1));
+}
+
+uint32_t route_bank(const cfg_t &c, uint32_t KY, uint32_t KX) {
+  if (c.dc == 4) return KY == 3 && KX == 3 ? BANK_W23 : 0;
+  if (c.dc != 5 || (uint32_t)c.dc_ky != KY || KX != KY) return 0;
+  if (KY == 5) return c.dc_s == 2 ? BANK_W25 : 0;
+  if (KY == 3) return c.dc_s == 4 ? BANK_W43 : BANK_W23;
+  return 0;
+}
+
+// the k-major bank, then the Winograd banks of the mask (cut to the kernel size's)
+int launch_pack_banks(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX,
+                      uint32_t banks, bool first, bool last) {
+  banks &= all_banks(KY, KX);
+  int rc = launch_xpose_filts(ctx, filts, packed, OC, IC, KY * KX, first, last && !banks);
+  for (uint32_t b = 1; rc == BH_OK && b <= BANK_W25; b <<= 1) {
+    if (!(banks & b)) continue;
+    float *u = packed + bank_offset(OC, IC, KY, KX, banks, b);
+    const bool lb = last && !(banks & ~(2 * b - 1));  // the mask's last bank
+    rc = b == BANK_W23 ? launch_wino_pack(ctx, filts, u, OC, IC, false, lb)
+                       : launch_wx_pack(ctx, filts, u, OC, IC, b == BANK_W25 ? 5 : 3, false, lb);
+  }
   return rc;
 }
 
@@ -987,13 +1005,14 @@ int ensure_wpack(bh_ctx *ctx, size_t bytes) {
 }  // namespace bhk
 
 namespace bh {
-// the k-major bank, then the Winograd banks of the kernel size (bhk::launch_pack_all)
-size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
-  return bhk::pack_floats(OC, IC, KY, KX);
+// the k-major bank, then the Winograd banks of the mask (bhk::launch_pack_banks)
+size_t conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks) {
+  return bhk::banks_floats(OC, IC, KY, KX, banks);
 }
 int launch_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
-                           uint32_t KX) {
-  if (conv_filts_packed_floats(OC, IC, KY, KX) * 4 >= 0x7fffffc0ull) return fail(BH_UNSUP, "conv_filts_pack: bank larger than 2 GiB");
-  return bhk::launch_pack_all(ctx, filts, packed, OC, IC, KY, KX, true, true);  // a call of its own
+                           uint32_t KX, uint32_t banks) {
+  if (conv_filts_packed_floats(OC, IC, KY, KX, banks) * 4 >= 0x7fffffc0ull)
+    return fail(BH_UNSUP, "conv_filts_pack: bank larger than 2 GiB");
+  return bhk::launch_pack_banks(ctx, filts, packed, OC, IC, KY, KX, banks, true, true);  // a call of its own
 }
 }  // namespace bh

@@ -302,6 +302,23 @@ int bh_conv2d_fwd_nchw_slab(bh_ctx *c, const float *in, const float *filts, cons
                          py, px, relu, out_chans_total);
 }
 
+int bh_conv2d_fwd_nchw_pkb(bh_ctx *c, const float *in, const float *filts, const float *packed, uint32_t banks,
+                           const float *biases, const float *res, float *out, uint32_t out_chans_total,
+                           uint32_t out_chan_ofs, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC,
+                           uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
+  BH_ENTER_CALL(c);
+  if (!in || !filts || !out) return bh::fail(BH_ERR, "null tensor");
+  if (!B || !IC || !H || !W || !OC || !KY || !KX || !sy || !sx)
+    return bh::fail(BH_UNSUP, "conv: zero-sized dimension or stride");
+  if (H + 2 * py < KY || W + 2 * px < KX) return bh::fail(BH_UNSUP, "conv: padded input smaller than kernel");
+  if (!out_chans_total) out_chans_total = OC;
+  if ((uint64_t)out_chan_ofs + OC > out_chans_total) return bh::fail(BH_ERR, "conv: output channel slab out of range");
+  if (res && out_chans_total != OC) return bh::fail(BH_ERR, "conv: residual and channel slab together");
+  const uint64_t ohw = (uint64_t)((H + 2 * py - KY) / sy + 1) * ((W + 2 * px - KX) / sx + 1);
+  return bh::launch_conv(c, in, filts, packed, biases, out + out_chan_ofs * ohw, B, IC, H, W, OC, KY, KX, sy, sx, py,
+                         px, relu, out_chans_total, res, false, false, banks);
+}
+
 int bh_conv2d_fwd_nchw(bh_ctx *c, const float *in, const float *filts, const float *biases, float *out,
                        uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY, uint32_t KX,
                        uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu) {
@@ -374,15 +391,31 @@ int bh_eltwise(bh_ctx *c, const float *a, const float *b, float *out, uint64_t n
 }
 
 size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX) {
-  return bh::conv_filts_packed_floats(OC, IC, KY, KX);
+  return bh::conv_filts_packed_floats(OC, IC, KY, KX, BH_BANKS_ALL);
 }
 
 int bh_conv_filts_pack(bh_ctx *c, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
                        uint32_t KX) {
+  return bh_conv_filts_pack_banks(c, filts, packed, OC, IC, KY, KX, BH_BANKS_ALL);
+}
+
+size_t bh_conv_filts_packed_floats_banks(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks) {
+  return bh::conv_filts_packed_floats(OC, IC, KY, KX, banks);
+}
+
+int bh_conv_filts_pack_banks(bh_ctx *c, const float *filts, float *packed, uint32_t OC, uint32_t IC, uint32_t KY,
+                             uint32_t KX, uint32_t banks) {
   BH_ENTER_CALL(c);
   if (!filts || !packed) return bh::fail(BH_ERR, "null tensor");
   if (!OC || !IC || !KY || !KX) return bh::fail(BH_UNSUP, "conv_filts_pack: zero-sized dimension");
-  return bh::launch_conv_filts_pack(c, filts, packed, OC, IC, KY, KX);
+  return bh::launch_conv_filts_pack(c, filts, packed, OC, IC, KY, KX, banks);
+}
+
+int bh_conv_route_banks(bh_ctx *c, const uint32_t *dims, uint32_t *banks) {
+  // c may be NULL: the tuning table's / heuristic's route (no device needed)
+  if (!dims || !banks) return bh::fail(BH_ERR, "null argument");
+  *banks = bh::conv_route_banks(c, dims);
+  return BH_OK;
 }
 
 int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
@@ -390,6 +423,17 @@ int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t n) {
   std::string s;
   if (op == 0) s = bh::sgemm_variant(dims[0], dims[1], dims[2]);
   else if (op == 1) s = bh::conv_variant(dims);
+  else return bh::fail(BH_ERR, "unknown op kind");
+  std::snprintf(buf, n, "%s", s.c_str());
+  return BH_OK;
+}
+
+int bh_variant_name_ctx(bh_ctx *c, int op, const uint32_t *dims, char *buf, size_t n) {
+  BH_ENTER(c);
+  if (!dims || !buf || !n) return bh::fail(BH_ERR, "null argument");
+  std::string s;
+  if (op == 0) s = bh::sgemm_variant_ctx(c, dims[0], dims[1], dims[2]);
+  else if (op == 1) s = bh::conv_variant_ctx(c, dims);
   else return bh::fail(BH_ERR, "unknown op kind");
   std::snprintf(buf, n, "%s", s.c_str());
   return BH_OK;

@@ -150,44 +150,6 @@ struct latex_rows_t {
   }
 };
 
-// comp_vars for one var pair (src/comp_util.cc:21-57 with ssds_diff_t, src/boda_base.cc:126-207)
-bool comp_var(std::ostream &out, std::string const &vn, dims_t const &dims, std::vector<float> const &o1,
-              std::vector<float> const &o2, double toler, uint32_t max_err, double *mrd_out) {
-  double ssds = 0, sds = 0, mad = 0, mrd = 0, s1 = 0, s2 = 0;
-  uint64_t ndiff = 0;
-  const size_t n = o1.size();
-  for (size_t i = 0; i < n; ++i) {
-    s1 += o1[i];
-    s2 += o2[i];
-    const double d = double(o2[i]) - double(o1[i]);
-    sds += d;
-    ssds += d * d;
-    mad = std::max(mad, std::fabs(d));
-    mrd = std::max(mrd, min_sig_mag_rel_diff(1.0, o1[i], o2[i]));
-    ndiff += o1[i] != o2[i];
-  }
-  const bool nan = std::isnan(ssds) || std::isnan(sds) || std::isnan(mad);
-  *mrd_out = nan ? NAN : mrd;
-  if (!(mrd >= toler || nan)) return false;
-  out << vn << ": DIMS[" << dims.str() << "] ssds_str(out_batch_1,out_batch_2)=cnt=" << ndiff
-      << " sum_squared_diffs=" << raw_str(ssds) << " avg_abs_diff=" << raw_str(std::sqrt(ssds / n))
-      << " max_abs_diff=" << raw_str(mad) << " sum_diffs=" << raw_str(sds) << " avg_diff=" << raw_str(sds / n)
-      << " max_rel_diff=" << raw_str(mrd) << " avg1=" << raw_str(s1 / n) << " avg2=" << raw_str(s2 / n) << "\n";
-  uint32_t nerr = 0;
-  for (size_t i = 0; i < n; ++i) {
-    if (std::fabs(min_sig_mag_rel_diff(1.0, o1[i], o2[i])) < toler) continue;
-    std::string ix;  // dims_t::ix_str: name=index per dim
-    size_t r = i;
-    for (size_t k = dims.d.size(); k-- > 0;) {
-      ix = dims.d[k].name + "=" + std::to_string(r % dims.d[k].sz) + (ix.empty() ? "" : ":") + ix;
-      r /= dims.d[k].sz;
-    }
-    out << "[" << ix << "]: v1=" << raw_str(o1[i]) << " v2=" << raw_str(o2[i]) << " \n";
-    if (++nerr > max_err) break;
-  }
-  return true;
-}
-
 void vcheck(int rc, char const *what) {
   if (rc != BHV_OK) rt_err(std::string(what) + ": " + bhv_last_error());
 }
@@ -224,7 +186,7 @@ int main(int argc, char **argv) {
     std::cerr << "usage: boda_hip_cnn_op_info --cnn-func-sigs-fn=F [--out-fn=F] [--op-info-tab-fn=F]\n"
                  "  [--op-eff-tab-fn=F] [--print-format=0|1|2] [--inc-op-info-in-eff=0] [--peak-flops=157.3e12]\n"
                  "  [--run-iter=1] [--graph-reps=0] [--gen-data-mode=5] [--comp=vendor|none] [--mrd-toler=2e-4]\n"
-                 "  [--max-err=10] [--wino-mrd-toler=2e-2] [--show-mrd=1] [--device=0]\n"
+                 "  [--max-err=10] [--wino-mrd-toler=2e-3] [--show-mrd=1] [--device=0]\n"
                  "  [--eff-comp=1] [--no-run=1] | --pp-vals=v,v,...\n";
     return 2;
   }
@@ -246,11 +208,11 @@ int main(int argc, char **argv) {
     const uint32_t graph_reps = std::stoul(o.get("graph-reps", "0"));
     const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
     const double toler = std::stod(o.get("mrd-toler", "2e-4"));
-    // Winograd routes (variant names *_wino_*) compare at their own tolerance, as ops-prof widens its
-    // compare for cuDNN's Winograd (src/rtc_prof.cc:314-319): the input / output transforms turn
-    // cancellation in the direct sum into element errors min_sig_mag_rel_diff sees on near-zero
-    // outputs (measured per op with --show-mrd=1)
-    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-2"));
+    // Winograd routes (variant names *_wino_*) compare at the reference's Winograd tolerance, 2e-3
+    // (ops-prof's widening for cuDNN's 3x3 Winograd, src/rtc_prof.cc:314-319): the input / output
+    // transforms turn cancellation in the direct sum into element errors min_sig_mag_rel_diff sees
+    // on near-zero outputs (measured per op with --show-mrd=1)
+    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-3"));
     const bool show_mrd = o.get("show-mrd", "0") != "0";
     const uint32_t max_err = std::stoul(o.get("max-err", "10"));
     const std::string comp = o.get("comp", "vendor");

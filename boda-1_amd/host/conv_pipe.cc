@@ -626,9 +626,20 @@ void conv_pipe_fwd_t::gen_op(conv_op_t const &op) {
     if (bias) args["biases"] = bv;
     if (ra != resadds.end()) args["res"] = ra->second.res;
     if (pack_filts && !ip) {
-      // Boda's xpose_filts at init (src/rtc_fwd.cc:306-326): the k-major bank the ring kernels read
+      // Boda's xpose_filts at init (src/rtc_fwd.cc:306-326): the k-major bank the ring kernels read,
+      // + the Winograd bank the conv's route reads (bh_conv_route_banks; pack_all_banks: all of them)
+      uint32_t banks = BH_BANKS_ALL;
+      if (!pack_all_banks) {
+        const uint32_t d[11] = {s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px};
+        if (bh_conv_route_banks(nullptr, d, &banks) != BH_OK) rt_err("bh_conv_route_banks: " + std::string(bh_last_error()));
+      }
+      fo.str_vals["hip_pack_banks"] = std::to_string(banks);
+      rtc->compile({{fn, "", {}, fo}}, rtc_compile_opts_t());  // the conv reads the same mask
+      const size_t nxp = bh_conv_filts_packed_floats_banks(s.OC, s.IC, s.KY, s.KX, banks);
+      pack_bytes += nxp * 4;
+      filt_bytes += (uint64_t)s.OC * s.IC * s.KY * s.KX * 4;
       std::string xv = op.tag + "_filts_xp";
-      rtc->create_var_with_dims(xv, vec_dims("v", (uint32_t)bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX)));
+      rtc->create_var_with_dims(xv, vec_dims("v", (uint32_t)nxp));
       std::string xfn = "hip_xpose_filts__" + op.tag;
       rtc->compile({{xfn, "", {}, fo}}, rtc_compile_opts_t());
       rtc_func_call_t xc;
@@ -762,6 +773,7 @@ void conv_pipe_fwd_t::init(p_conv_pipe_t const &cp_, nesi_init_arg_t *const nia)
   per_call_fn = a.get_str("per_call_fn", "");
   graph_reps = a.get_u32("graph_reps", 0);
   pack_filts = a.get_bool("pack_filts", true);
+  pack_all_banks = a.get_bool("pack_all_banks", false);
   fold_affines = a.get_bool("fold_affines", true);
   concat_in_place = a.get_bool("concat_in_place", true);
   fuse_residual = a.get_bool("fuse_residual", true);
@@ -894,6 +906,10 @@ std::string conv_pipe_fwd_t::get_info_log(void) {
                times.size(), graph_reps, graph_ms, graph_ms > 0 ? flops / graph_ms / 1e6 : 0.0);
       ret += buf;
     }
+    snprintf(buf, sizeof(buf), "resident filter packs %.1f MB (%.2fx the %.1f MB of filters%s)\n", pack_bytes / 1e6,
+             filt_bytes ? (double)pack_bytes / filt_bytes : 0.0, filt_bytes / 1e6,
+             pack_all_banks ? ", every Winograd bank" : ", the banks each route reads");
+    ret += buf;
   }
   for (auto const &vn : dump_vars) {
     p_nda_t n = rtc->create_nda_from_var(vn);

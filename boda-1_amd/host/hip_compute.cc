@@ -70,7 +70,20 @@ struct var_info_t {
 
 struct call_ev_t {
   int b, e;
+  std::string variant;  // the kernel variant a hot call (hip_conv / hip_sgemm) ran
 };
+
+// index of the kernel configuration named n for op kind (0 sgemm, 1 conv), by bh_tune_cfg_name
+int cfg_index_of(int op, std::string const &n) {
+  static std::map<std::pair<int, std::string>, int> cache;
+  auto it = cache.find({op, n});
+  if (it != cache.end()) return it->second;
+  char buf[128];
+  for (int i = 0; bh_tune_cfg_name(op, i, buf, sizeof buf) == BH_OK; ++i)
+    if (n == buf) return cache[{op, n}] = i;
+  unsup_err(std::string("op_tune: no ") + (op ? "conv" : "sgemm") + " configuration named '" + n + "'");
+  return -1;
+}
 
 struct hip_compute_t : public rtc_compute_t {
   int device;
@@ -199,6 +212,45 @@ struct hip_compute_t : public rtc_compute_t {
     return (uint32_t)(calls.size() - 1);
   }
 
+  // the op's tune (add_hip_annotations(op, tune)) applied to the context for one call, then the
+  // table's choice restored
+  struct tune_guard_t {
+    bh_ctx *ctx;
+    int op;
+    bool cfg = false, wt = false;
+    tune_guard_t(bh_ctx *c, int o, op_base_t const &fop) : ctx(c), op(o) {
+      auto sv = [&](char const *k) -> std::string const * {
+        auto it = fop.str_vals.find(k);
+        return it == fop.str_vals.end() ? nullptr : &it->second;
+      };
+      if (std::string const *n = sv("hip_cfg")) {
+        std::string const *sp = sv("hip_splits");
+        bh_check(bh_tune_set(ctx, op, cfg_index_of(op, *n), sp ? std::stoi(*sp) : 0), "bh_tune_set");
+        cfg = true;
+      } else if (sv("hip_splits")) {
+        rt_err("op_tune: splits without cfg");
+      }
+      if (std::string const *w = sv("hip_wt")) {
+        bh_check(bh_tune_set_policy(ctx, op, std::stoi(*w)), "bh_tune_set_policy");
+        wt = true;
+      }
+    }
+    ~tune_guard_t() {
+      if (cfg) (void)bh_tune_set(ctx, op, -1, 0);
+      if (wt) (void)bh_tune_set_policy(ctx, op, -1);
+    }
+  };
+  // the Winograd banks a pack of this op holds (op str_vals hip_pack_banks, a BH_BANK_* mask;
+  // default: every bank of the kernel size, bh_conv_filts_pack's layout)
+  static uint32_t pack_banks_of(op_base_t const &op) {
+    auto it = op.str_vals.find("hip_pack_banks");
+    return it == op.str_vals.end() ? BH_BANKS_ALL : (uint32_t)std::stoul(it->second);
+  }
+  std::string variant_of(int op, uint32_t const *d) {
+    char buf[192];
+    return bh_variant_name_ctx(ctx, op, d, buf, sizeof buf) == BH_OK ? std::string(buf) : std::string();
+  }
+
   float *arg_ptr(rtc_func_call_t const &rfc, std::string const &an, bool optional = false) {
     auto it = rfc.arg_map.find(an);
     if (it == rfc.arg_map.end()) {
@@ -300,40 +352,45 @@ struct hip_compute_t : public rtc_compute_t {
       dims_t const &a = arg_dims(rfc, "a"), &b = arg_dims(rfc, "b");
       uint32_t M = a.dsz("M"), K = a.dsz("K"), N = b.dsz("N");
       if (b.dsz("K") != K) rt_err("hip_sgemm: a/b K mismatch");
+      tune_guard_t tg(ctx, 0, fi.op);
       bh_check(bh_sgemm_kmajor(ctx, arg_ptr(rfc, "a"), arg_ptr(rfc, "b"), arg_ptr(rfc, "c"), M, N, K), "hip_sgemm");
+      const uint32_t d[3] = {M, N, K};
+      ev.variant = variant_of(0, d);
     } else if (kind == "hip_conv") {
       conv_shape_t s = get_conv_shape(fi.op);
+      tune_guard_t tg(ctx, 1, fi.op);
+      const uint32_t d[11] = {s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px};
+      ev.variant = variant_of(1, d);
       auto r = fi.op.scalars.find("conv_has_relu");
       int relu = r == fi.op.scalars.end() ? 1 : (int)r->second;
-      // filts_xp (optional): the bank hip_xpose_filts made before the timed calls
+      // filts_xp (optional): the pack hip_xpose_filts made before the timed calls, holding the
+      // banks of the op's hip_pack_banks mask; res (optional): a fused residual add; out_chan_ofs
+      // (optional): the conv writes its channel slab of a wider output in place
       auto oc0 = fi.op.scalars.find("out_chan_ofs");
       float *res = arg_ptr(rfc, "res", true);
-      if (res) {  // residual add (a fused Eltwise SUM) in the conv epilogue
+      uint32_t octot = 0, ofs = 0;
+      if (res) {
         if (oc0 != fi.op.scalars.end()) rt_err(fn + ": residual and channel slab together");
         if (arg_dims(rfc, "res") != arg_dims(rfc, "out")) rt_err(fn + ": res / out dims differ");
-        bh_check(bh_conv2d_fwd_nchw_res(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
-                                        arg_ptr(rfc, "biases", true), res, arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W,
-                                        s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
-                 "hip_conv");
-      } else if (oc0 == fi.op.scalars.end()) {
-        bh_check(bh_conv2d_fwd_nchw_pk(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
-                                       arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), s.B, s.IC, s.H, s.W, s.OC,
-                                       s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
-                 "hip_conv");
-      } else {  // a channel slab of a wider output (a Concat's, written in place)
+      } else if (oc0 != fi.op.scalars.end()) {
         uint32_t OB, OCT, OH, OW;
         nchw("out", OB, OCT, OH, OW);
         if (OB != s.B || OH != s.OH || OW != s.OW) rt_err(fn + ": out dims do not match the conv");
-        bh_check(bh_conv2d_fwd_nchw_slab(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
-                                         arg_ptr(rfc, "biases", true), arg_ptr(rfc, "out"), OCT, (uint32_t)oc0->second,
-                                         s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
-                 "hip_conv");
+        octot = OCT;
+        ofs = (uint32_t)oc0->second;
       }
+      bh_check(bh_conv2d_fwd_nchw_pkb(ctx, arg_ptr(rfc, "in"), arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp", true),
+                                      pack_banks_of(fi.op), arg_ptr(rfc, "biases", true), res, arg_ptr(rfc, "out"),
+                                      octot, ofs, s.B, s.IC, s.H, s.W, s.OC, s.KY, s.KX, s.sy, s.sx, s.py, s.px, relu),
+               "hip_conv");
     } else if (kind == "hip_xpose_filts") {  // Boda's xpose_filts (test/rtc/xpose_filts.cucl) for hip_conv
+      // the k-major bank + the Winograd banks of the op's hip_pack_banks mask (default: all of them)
       conv_shape_t s = get_conv_shape(fi.op);
-      if (arg_dims(rfc, "filts_xp").elems() != bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX))
+      const uint32_t banks = pack_banks_of(fi.op);
+      if (arg_dims(rfc, "filts_xp").elems() != bh_conv_filts_packed_floats_banks(s.OC, s.IC, s.KY, s.KX, banks))
         rt_err("hip_xpose_filts: filts_xp has the wrong size");
-      bh_check(bh_conv_filts_pack(ctx, arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp"), s.OC, s.IC, s.KY, s.KX),
+      bh_check(bh_conv_filts_pack_banks(ctx, arg_ptr(rfc, "filts"), arg_ptr(rfc, "filts_xp"), s.OC, s.IC, s.KY, s.KX,
+                                        banks),
                "hip_xpose_filts");
     } else {  // gen_data_<type>_<arg>
       std::string an = fn.substr(fn.rfind('_') + 1);
@@ -361,6 +418,11 @@ struct hip_compute_t : public rtc_compute_t {
     calls.clear();
     bh_check(bh_events_reset(ctx), "bh_events_reset");
   }
+  std::string get_call_variant(uint32_t const &call_id) override {
+    if (call_id >= calls.size()) rt_err("get_call_variant: bad call id");
+    return calls[call_id].variant;
+  }
+
   float get_dur(uint32_t const &b, uint32_t const &e) override {
     if (b >= calls.size() || e >= calls.size()) rt_err("get_dur: bad call id");
     float ms = 0;

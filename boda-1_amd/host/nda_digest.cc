@@ -9,6 +9,7 @@
 #include <ostream>
 #include <random>
 #include <set>
+#include <sstream>
 
 namespace boda_hip {
 
@@ -258,6 +259,52 @@ void write_wisdom(std::ostream &out, op_wisdom_t const &w) {
     out << "/op_tune_wisdom_t\n";
   }
   out << "/op_wisdom_t\n";
+}
+
+namespace {
+std::string num_str(double v) {  // str(double) of the reference: a default ostream (src/str_util.H:107-111)
+  std::ostringstream s;
+  s << v;
+  return s.str();
+}
+}  // namespace
+
+// comp_vars for one var pair (src/comp_util.cc:21-57 with ssds_diff_t, src/boda_base.cc:126-207)
+bool comp_var(std::ostream &out, std::string const &vn, dims_t const &dims, std::vector<float> const &o1,
+              std::vector<float> const &o2, double toler, uint32_t max_err, double *mrd_out) {
+  double ssds = 0, sds = 0, mad = 0, mrd = 0, s1 = 0, s2 = 0;
+  uint64_t ndiff = 0;
+  const size_t n = o1.size();
+  for (size_t i = 0; i < n; ++i) {
+    s1 += o1[i];
+    s2 += o2[i];
+    const double d = double(o2[i]) - double(o1[i]);
+    sds += d;
+    ssds += d * d;
+    mad = std::max(mad, std::fabs(d));
+    mrd = std::max(mrd, min_sig_mag_rel_diff(1.0, o1[i], o2[i]));
+    ndiff += o1[i] != o2[i];
+  }
+  const bool nan = std::isnan(ssds) || std::isnan(sds) || std::isnan(mad);
+  *mrd_out = nan ? NAN : mrd;
+  if (!(mrd >= toler || nan)) return false;
+  out << vn << ": DIMS[" << dims.str() << "] ssds_str(out_batch_1,out_batch_2)=cnt=" << ndiff
+      << " sum_squared_diffs=" << num_str(ssds) << " avg_abs_diff=" << num_str(std::sqrt(ssds / n))
+      << " max_abs_diff=" << num_str(mad) << " sum_diffs=" << num_str(sds) << " avg_diff=" << num_str(sds / n)
+      << " max_rel_diff=" << num_str(mrd) << " avg1=" << num_str(s1 / n) << " avg2=" << num_str(s2 / n) << "\n";
+  uint32_t nerr = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (std::fabs(min_sig_mag_rel_diff(1.0, o1[i], o2[i])) < toler) continue;
+    std::string ix;  // dims_t::ix_str: name=index per dim
+    size_t r = i;
+    for (size_t k = dims.d.size(); k-- > 0;) {
+      ix = dims.d[k].name + "=" + std::to_string(r % dims.d[k].sz) + (ix.empty() ? "" : ":") + ix;
+      r /= dims.d[k].sz;
+    }
+    out << "[" << ix << "]: v1=" << num_str(o1[i]) << " v2=" << num_str(o2[i]) << " \n";
+    if (++nerr > max_err) break;
+  }
+  return true;
 }
 
 }  // namespace boda_hip

@@ -179,4 +179,43 @@ void add_hip_annotations(op_base_t &op) {
   unsup_err("hip backend: no kernel for op type '" + op.type + "'");
 }
 
+std::string hip_op_tune_t::str() const {
+  std::string r;
+  auto add = [&](std::string const &k, std::string const &v) { r += (r.empty() ? "" : ",") + k + "=" + v; };
+  if (!use_be.empty()) add("use_be", use_be);
+  if (!cfg.empty()) add("cfg", cfg);
+  if (splits) add("splits", std::to_string(splits));
+  if (wt >= 0) add("wt", std::to_string(wt));
+  return "(" + r + ")";
+}
+
+hip_op_tune_t parse_hip_op_tune(std::string const &s) {
+  p_lexp_t l = parse_lexp(s);
+  hip_op_tune_t t;
+  if (!l->is_list) rt_err("op_tune: expected a (k=v,...) list, got '" + s + "'");
+  for (auto const &kv : l->kids) {
+    if (kv.second->is_list) rt_err("op_tune: field '" + kv.first + "' is a list");
+    std::string const &v = kv.second->leaf;
+    try {
+      if (kv.first == "use_be") t.use_be = v;
+      else if (kv.first == "cfg") t.cfg = v;
+      else if (kv.first == "splits") t.splits = std::stoi(v);
+      else if (kv.first == "wt") t.wt = std::stoi(v);
+      else rt_err("op_tune: unknown field '" + kv.first + "' (use_be, cfg, splits, wt)");
+    } catch (std::logic_error const &) {
+      rt_err("op_tune: bad value '" + v + "' for " + kv.first);
+    }
+  }
+  if (!t.use_be.empty() && t.use_be != "hip") unsup_err("op_tune: use_be=" + t.use_be + " is not this backend");
+  if (t.wt < -1 || t.wt > 1) rt_err("op_tune: wt must be -1, 0 or 1");
+  return t;
+}
+
+void add_hip_annotations(op_base_t &op, hip_op_tune_t const &tune) {
+  add_hip_annotations(op);
+  if (!tune.cfg.empty()) op.str_vals["hip_cfg"] = tune.cfg;
+  if (tune.splits) op.str_vals["hip_splits"] = std::to_string(tune.splits);
+  if (tune.wt >= 0) op.str_vals["hip_wt"] = std::to_string(tune.wt);
+}
+
 }  // namespace boda_hip

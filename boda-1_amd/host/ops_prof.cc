@@ -1,13 +1,18 @@
 // ops_prof.cc -- boda_hip_ops_prof: Boda's per-op profiling sweep (ops-prof,
 // src/rtc_prof.cc:139-371 with profile_rcg_call :44-126) over be=hip.
 //
-// For each op of an op list (either dialect): annotate it for the hip backend,
-// create its vars (zero-filled), fill the inputs with gen_data on the device,
-// run the main kernel --run-iter times, take the event-timed duration of the
-// last call, digest every output (seed = std::hash of the var name) and compare
-// it with the known-good digest of --wisdom-in-fn using the reference's own
-// mrd_comp, write --wisdom-out-fn (kg digests, and runs with --write-runs=1) and
-// print ***ALL IS WELL*** or ***MAD FAILS***, as the reference does.
+// For each op of an op list (either dialect) and each tune of --op-tunes (the known-good tune
+// --kg-tune-tag first, then the others in tag order; default one tune, the tuning table's
+// choice): annotate it for the hip backend with the tune (a kernel configuration, its K splits
+// and store policy, forced through bh_tune_set), create its vars (zero-filled), fill the inputs
+// with gen_data on the device, run the main kernel --run-iter times, take the event-timed
+// duration of the last call; compare every output element-wise with the known-good tune's
+// (comp_vars, src/rtc_prof.cc:276-321) at --mrd-toler, or the per-function --func-mrd-toler of
+// the kernel variant the call ran (Winograd variants: 2e-3, the reference's Winograd widening,
+// :314-319); digest it (seed = std::hash of the var name) and compare it with the known-good
+// digest of --wisdom-in-fn using the reference's own mrd_comp at the same tolerance; write
+// --wisdom-out-fn (the kg tune's digests, and every tune's runs with --write-runs=1) and print
+// ***ALL IS WELL*** or ***MAD FAILS***, as the reference does.
 // --shard=k/n runs only the ops a greedy LPT partition (by roofline time) gives
 // to shard k of n, so n processes (one per GPU, --device=k) split a list with no
 // communication at all.
@@ -21,6 +26,7 @@
 #include <sstream>
 
 #include "boda_hip.h"
+#include "lexp.H"
 #include "nda_digest.H"
 #include "op_desc.H"
 #include "rtc_compute.H"
@@ -164,15 +170,62 @@ int main(int argc, char **argv) {
     }
     if (ops_fn.empty()) {
       std::cerr << "usage: boda_hip_ops_prof --ops-fn=F [--wisdom-in-fn=F] [--wisdom-out-fn=F] [--out-fn=F]\n"
+                   "  [--op-tunes='(tag=(use_be=hip,cfg=NAME,splits=N,wt=W),...)'] [--kg-tune-tag=tag]\n"
+                   "  [--func-mrd-toler='(variant-or-word=toler,...)'] [--wino-mrd-toler=2e-3] [--max-err=10]\n"
                    "  [--gen-data-mode=5] [--run-iter=1] [--mrd-toler=2e-4] [--device=0] [--write-runs=0]\n"
+                   "  [--write-kg-digest=1]\n"
                    "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F | --list-shard=k/n --ops-fn=F\n";
       return 2;
     }
     const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
     const uint32_t run_iter = std::max(1ul, std::stoul(o.get("run-iter", "1")));
     const double mrd = std::stod(o.get("mrd-toler", "2e-4"));
+    const uint32_t max_err = std::stoul(o.get("max-err", "10"));
     const bool write_runs = o.get("write-runs", "0") != "0";
+    const bool write_kg_digest = o.get("write-kg-digest", "1") != "0";
     uint32_t skip = std::stoul(o.get("skip-ops", "0"));
+    // --op-tunes (a tag -> op_tune map, iterated in tag order as the reference's map_str_op_tune_t)
+    // and --kg-tune-tag (src/rtc_prof.cc:151,166): the kg tune runs first; its outputs are the lhs
+    // of a full-data comp_vars against every tune, itself included (:276-321)
+    std::map<std::string, hip_op_tune_t> tunes;
+    {
+      p_lexp_t l = parse_lexp(o.get("op-tunes", "(hip=(use_be=hip))"));
+      if (!l->is_list || l->kids.empty()) rt_err("--op-tunes wants (tag=(k=v,...),...)");
+      for (auto const &kv : l->kids) {
+        if (tunes.count(kv.first)) rt_err("--op-tunes: duplicate tag " + kv.first);
+        tunes[kv.first] = parse_hip_op_tune(kv.second->str());
+      }
+    }
+    std::string kg_tag = o.get("kg-tune-tag");
+    if (kg_tag.empty()) {
+      if (tunes.size() != 1) rt_err("--kg-tune-tag is required with more than one tune");
+      kg_tag = tunes.begin()->first;
+    }
+    if (!tunes.count(kg_tag)) rt_err("--kg-tune-tag=" + kg_tag + " names no tune of --op-tunes");
+    std::vector<std::string> order{kg_tag};
+    for (auto const &kv : tunes)
+      if (kv.first != kg_tag) order.push_back(kv.first);
+    // --func-mrd-toler=(key=toler,...): per-function tolerance (src/rtc_prof.cc:160,312). The
+    // function is the kernel variant a call ran (bh_variant_name_ctx); a key applies when it equals
+    // the variant or is one of its '_'-separated words (wino, dm, k1s, ...), the longest key wins.
+    std::map<std::string, double> func_toler;
+    {
+      p_lexp_t l = parse_lexp(o.get("func-mrd-toler", "()"));
+      for (auto const &kv : l->kids) func_toler[kv.first] = std::stod(kv.second->leaf);
+    }
+    // Winograd routes widen to 2e-3, the reference's widening for cuDNN's 3x3 Winograd
+    // (src/rtc_prof.cc:314-319), unless --func-mrd-toler names them
+    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-3"));
+    auto toler_of = [&](std::string const &variant) {
+      double t = mrd;
+      size_t best = 0;
+      for (auto const &kv : func_toler) {
+        const bool hit = variant == kv.first || ("_" + variant + "_").find("_" + kv.first + "_") != std::string::npos;
+        if (hit && kv.first.size() > best) best = kv.first.size(), t = kv.second;
+      }
+      if (!best && variant.find("_wino_") != std::string::npos) t = wino_toler;
+      return t;
+    };
     std::ofstream fout;
     std::ostream *out = &std::cout;
     if (!o.get("out-fn").empty()) {
@@ -196,9 +249,12 @@ int main(int argc, char **argv) {
     p_rtc_compute_t rtc = make_hip_compute(std::stoi(o.get("device", "0")));
     rtc->init();
     const std::string plat = rtc->get_plat_tag();
-    const std::string tune = "(use_be=hip)";
-    uint32_t num_fail = 0, n_run = 0, n_unsup = 0;
-    double sum_flops = 0, sum_secs = 0, sum_roof = 0;
+    uint32_t num_mad_fail = 0, n_unsup = 0;
+    struct agg_t {
+      uint32_t n = 0;
+      double flops = 0, secs = 0, roof = 0;
+    };
+    std::map<std::string, agg_t> agg;
     for (size_t ix = 0; ix < lines.size(); ++ix) {
       op_wisdom_t wi;
       bool have_wi = win.is_open() && read_next_wisdom(win, wi);
@@ -206,126 +262,171 @@ int main(int argc, char **argv) {
         --skip;
         continue;
       }
-      op_base_t op = parse_op_line(lines[ix]);
-      if (have_wi && !same_op(parse_op_line(wi.op_line), op)) rt_err("op mismatch between input wisdom and ops-list at op " + std::to_string(ix));
+      op_base_t op0 = parse_op_line(lines[ix]);
+      if (have_wi && !same_op(parse_op_line(wi.op_line), op0)) rt_err("op mismatch between input wisdom and ops-list at op " + std::to_string(ix));
       if (!mine[ix]) continue;
       op_wisdom_t wo;
       wo.op_line = lines[ix];
-      op_run_t run;
-      run.plat_tag = plat;
-      std::ostringstream err, err_extra;
-      std::map<std::string, p_nda_t> outs;
-      try {
-        add_hip_annotations(op);
-        std::vector<rtc_func_info_t> fis{{op.func_name, "", {}, op}};
-        for (auto const &vn : in_vars(op)) fis.push_back({"gen_data_" + op.type + "_" + vn, "", {}, op});
-        rtc->compile(fis, rtc_compile_opts_t());
-        for (auto const &vn : arg_vars(op)) rtc->create_var_with_dims(vn, op.get_dims(vn));
-        for (auto const &vn : in_vars(op)) {
-          rtc_func_call_t g;
-          g.rtc_func_name = "gen_data_" + op.type + "_" + vn;
-          g.arg_map[vn] = vn;
-          g.arg_map["mode"] = rtc_arg_t::val(mode);
-          g.arg_map["vi"] = rtc_arg_t::val(0.0);
-          rtc->run(g);
+      bool op_seen_errs = false;  // the op is printed once, before its first error (on_op_err)
+      std::map<std::string, p_nda_t> vs_kg;
+      bool have_kg = false;
+      for (std::string const &tag : order) {
+        hip_op_tune_t const &tune = tunes[tag];
+        op_base_t op = op0;
+        op_run_t run;
+        run.plat_tag = plat;
+        std::ostringstream err, err_extra;
+        std::map<std::string, p_nda_t> outs;
+        std::string variant;
+        try {
+          add_hip_annotations(op, tune);
+          std::vector<rtc_func_info_t> fis{{op.func_name, "", {}, op}};
+          for (auto const &vn : in_vars(op)) fis.push_back({"gen_data_" + op.type + "_" + vn, "", {}, op});
+          rtc->compile(fis, rtc_compile_opts_t());
+          for (auto const &vn : arg_vars(op)) rtc->create_var_with_dims(vn, op.get_dims(vn));
+          for (auto const &vn : in_vars(op)) {
+            rtc_func_call_t g;
+            g.rtc_func_name = "gen_data_" + op.type + "_" + vn;
+            g.arg_map[vn] = vn;
+            g.arg_map["mode"] = rtc_arg_t::val(mode);
+            g.arg_map["vi"] = rtc_arg_t::val(0.0);
+            rtc->run(g);
+          }
+          rtc_func_call_t c;
+          c.rtc_func_name = op.func_name;
+          for (auto const &vn : arg_vars(op)) c.arg_map[vn] = vn;
+          if (op.type == "Convolution") {
+            // layout transform of the filters before the timed calls, as the reference's
+            // xpose_filts (src/rtc_prof.cc:93-99; untimed)
+            conv_shape_t s = get_conv_shape(op);
+            rtc->compile({{"hip_xpose_filts", "", {}, op}}, rtc_compile_opts_t());
+            const uint32_t nxp = (uint32_t)bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX);
+            rtc->create_var_with_dims("filts_xp", dims_t(std::vector<std::pair<std::string, uint32_t>>{{"x", nxp}}));
+            rtc_func_call_t x;
+            x.rtc_func_name = "hip_xpose_filts";
+            x.arg_map["filts"] = "filts";
+            x.arg_map["filts_xp"] = "filts_xp";
+            rtc->run(x);
+            c.arg_map["filts_xp"] = "filts_xp";
+          }
+          uint32_t call_id = 0;
+          for (uint32_t r = 0; r < run_iter; ++r) call_id = rtc->run(c);
+          rtc->finish_and_sync();
+          run.rt_secs = rtc->get_dur(call_id, call_id) / 1000.0;
+          variant = rtc->get_call_variant(call_id);
+          for (auto const &vn : out_vars(op)) outs[vn] = rtc->create_nda_from_var(vn);
+          run.op_line = op.line;
+        } catch (unsup_exception const &e) {
+          err << "profile call failure: " << e.what();
+          ++n_unsup;  // recorded, not a MAD failure (src/rtc_prof.cc:287-296, :368-369)
         }
-        rtc_func_call_t c;
-        c.rtc_func_name = op.func_name;
-        for (auto const &vn : arg_vars(op)) c.arg_map[vn] = vn;
+        for (auto const &vn : arg_vars(op))
+          if (op.has_dims(vn)) {
+            try {
+              rtc->release_var(vn);
+            } catch (rt_exception const &) {
+            }
+          }
         if (op.type == "Convolution") {
-          // layout transform of the filters before the timed calls, as the reference's
-          // xpose_filts (src/rtc_prof.cc:93-99; untimed)
-          conv_shape_t s = get_conv_shape(op);
-          rtc->compile({{"hip_xpose_filts", "", {}, op}}, rtc_compile_opts_t());
-          const uint32_t nxp = (uint32_t)bh_conv_filts_packed_floats(s.OC, s.IC, s.KY, s.KX);
-          rtc->create_var_with_dims("filts_xp", dims_t(std::vector<std::pair<std::string, uint32_t>>{{"x", nxp}}));
-          rtc_func_call_t x;
-          x.rtc_func_name = "hip_xpose_filts";
-          x.arg_map["filts"] = "filts";
-          x.arg_map["filts_xp"] = "filts_xp";
-          rtc->run(x);
-          c.arg_map["filts_xp"] = "filts_xp";
-        }
-        uint32_t call_id = 0;
-        for (uint32_t r = 0; r < run_iter; ++r) call_id = rtc->run(c);
-        rtc->finish_and_sync();
-        run.rt_secs = rtc->get_dur(call_id, call_id) / 1000.0;
-        for (auto const &vn : out_vars(op)) outs[vn] = rtc->create_nda_from_var(vn);
-        run.op_line = op.line;
-      } catch (unsup_exception const &e) {
-        err << "profile call failure: " << e.what();
-        ++n_unsup;  // recorded, not a MAD failure (src/rtc_prof.cc:287-296, :368-369)
-      }
-      for (auto const &vn : arg_vars(op))
-        if (op.has_dims(vn)) {
           try {
-            rtc->release_var(vn);
+            rtc->release_var("filts_xp");
           } catch (rt_exception const &) {
           }
         }
-      if (op.type == "Convolution") {
-        try {
-          rtc->release_var("filts_xp");
-        } catch (rt_exception const &) {
-        }
-      }
-      rtc->release_per_call_id_data();
-      rtc->release_all_funcs();
-      std::string dstat = "n/a";
-      if (err.str().empty()) {
-        for (auto const &kv : outs) {
-          nda_digest_t d = nda_digest_t::make(kv.second->elems(), kv.second->dims, digest_seed_for(kv.first));
-          wo.kgs.emplace_back(kv.first, d);
-          if (have_wi) {
-            dstat = "ok";
-            for (auto const &kg : wi.kgs)
-              if (kg.first == kv.first) {
-                double worst = 0;
-                std::string cr = kg.second.mrd_comp(d, mrd, &worst);
-                if (!cr.empty()) {
-                  dstat = "FAIL";
-                  err << kv.first << " digest mrd_comp() failure vs stored digest (worst rd/tol "
-                      << worst << ")";
-                  err_extra << "comp_res:\n" << cr;
-                }
-              }
+        rtc->release_per_call_id_data();
+        rtc->release_all_funcs();
+        if (tag == kg_tag) {  // the known-good run: the lhs of the compares, and the digests
+          if (!err.str().empty()) {
+            err << " known-good op_tune (kg_tune_tag=" << kg_tag << ") failed. Can't write digests or do live comparisons.";
+          } else {
+            vs_kg = outs;
+            have_kg = true;
+            if (write_kg_digest)
+              for (auto const &kv : outs)
+                wo.kgs.emplace_back(kv.first, nda_digest_t::make(kv.second->elems(), kv.second->dims,
+                                                                 digest_seed_for(kv.first)));
           }
         }
-        op_work_t w = op_work(op);
-        sum_flops += w.flops;
-        sum_secs += run.rt_secs;
-        sum_roof += roofline_secs(w);
-        ++n_run;
-        char buf[512];
-        std::snprintf(buf, sizeof(buf), "op_ix=%zu func=%s secs=%.6e gflops=%.1f roofline=%.1f%% digest=%s\n", ix,
-                      op.func_name.c_str(), run.rt_secs, w.flops / run.rt_secs / 1e9,
-                      100.0 * roofline_secs(w) / run.rt_secs, dstat.c_str());
-        *out << buf;
+        std::string dstat = "n/a", cstat = "n/a";
+        double worst_mrd = 0;
+        if (err.str().empty()) {
+          const double vmt = toler_of(variant);
+          if (have_kg) {  // full-data compare against the known-good run
+            cstat = "ok";
+            for (auto const &kv : vs_kg) {
+              auto it = outs.find(kv.first);
+              if (it == outs.end()) rt_err("reg/comp out var set mismatch for tune " + tag);
+              double m = 0;
+              std::ostringstream cv;
+              if (comp_var(cv, kv.first, kv.second->dims, *kv.second->data, *it->second->data, vmt, max_err, &m)) {
+                ++num_mad_fail;
+                cstat = "FAIL";
+                err << cv.str();
+              }
+              worst_mrd = std::max(worst_mrd, m);
+            }
+          }
+          if (have_wi) {  // digest compare against the stored known-good digests
+            dstat = "ok";
+            for (auto const &kv : outs) {
+              nda_digest_t d = nda_digest_t::make(kv.second->elems(), kv.second->dims, digest_seed_for(kv.first));
+              for (auto const &kg : wi.kgs)
+                if (kg.first == kv.first) {
+                  double worst = 0;
+                  std::string cr = kg.second.mrd_comp(d, vmt, &worst);
+                  if (!cr.empty()) {
+                    dstat = "FAIL";
+                    err << kv.first << " digest mrd_comp() failure vs stored digest (worst rd/tol " << worst << ")";
+                    err_extra << "comp_res:\n" << cr;
+                  }
+                }
+            }
+            if (dstat == "FAIL") ++num_mad_fail;
+          }
+          op_work_t w = op_work(op);
+          agg_t &g = agg[tag];
+          g.flops += w.flops;
+          g.secs += run.rt_secs;
+          g.roof += roofline_secs(w);
+          ++g.n;
+          char buf[640];
+          std::snprintf(buf, sizeof(buf),
+                        "op_ix=%zu tune=%s func=%s secs=%.6e gflops=%.1f roofline=%.1f%% mrd_vs_kg=%.3e toler=%.1e "
+                        "comp=%s digest=%s\n",
+                        ix, tag.c_str(), variant.empty() ? op.func_name.c_str() : variant.c_str(), run.rt_secs,
+                        w.flops / run.rt_secs / 1e9, 100.0 * roofline_secs(w) / run.rt_secs, worst_mrd, vmt,
+                        cstat.c_str(), dstat.c_str());
+          *out << buf;
+        }
+        run.err = err.str();
+        if (!run.err.empty()) {
+          if (!op_seen_errs) *out << "-----\n errors for op_ix=" << ix << " op='" << lines[ix] << "'\n";
+          op_seen_errs = true;
+          *out << "--  comp fail for op_tune='" << tune.str() << "'\n" << run.err << "\n" << err_extra.str();
+        }
+        if (write_runs) wo.tunes.push_back({tune.str(), {run}});
       }
-      run.err = err.str();
-      if (!run.err.empty()) {
-        if (dstat == "FAIL") ++num_fail;
-        *out << "-----\n errors for op_ix=" << ix << " op='" << lines[ix] << "'\n--  comp fail for op_tune='" << tune
-             << "'\n" << run.err << "\n" << err_extra.str();
-      }
+      if (!write_kg_digest && have_wi) wo.kgs = wi.kgs;
       if (wout.is_open()) {
-        if (write_runs) wo.tunes.push_back({tune, {run}});
         write_wisdom(wout, wo);
         wout.flush();
       }
       out->flush();
     }
-    if (n_run) {
-      char buf[256];
-      std::snprintf(buf, sizeof(buf), "summary: ops=%u sum_gflop=%.3f sum_kernel_ms=%.4f agg_gflops=%.1f roofline_frac=%.4f plat=%s\n",
-                    n_run, sum_flops / 1e9, sum_secs * 1e3, sum_flops / sum_secs / 1e9, sum_roof / sum_secs,
-                    plat.c_str());
+    for (std::string const &tag : order) {
+      agg_t const &g = agg[tag];
+      if (!g.n) continue;
+      char buf[320];
+      std::snprintf(buf, sizeof(buf),
+                    "summary: ops=%u sum_gflop=%.3f sum_kernel_ms=%.4f agg_gflops=%.1f roofline_frac=%.4f plat=%s "
+                    "tune=%s\n",
+                    g.n, g.flops / 1e9, g.secs * 1e3, g.flops / g.secs / 1e9, g.roof / g.secs, plat.c_str(), tag.c_str());
       *out << buf;
     }
     if (n_unsup) *out << "unsupported (recorded in wisdom, skipped): " << n_unsup << "\n";
-    if (!num_fail) *out << "***ALL IS WELL***\n";
-    else *out << "***MAD FAILS*** num_mad_fail=" << num_fail << "\n";
-    return num_fail ? 1 : 0;
+    if (!num_mad_fail) *out << "***ALL IS WELL***\n";
+    else *out << "***MAD FAILS*** num_mad_fail=" << num_mad_fail << "\n";
+    return num_mad_fail ? 1 : 0;
   } catch (rt_exception const &e) {
     std::cerr << "error: " << e.what() << "\n";
     return 3;

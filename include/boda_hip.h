@@ -38,7 +38,7 @@ extern "C" {
 #define BH_ERR 1
 #define BH_UNSUP 2
 
-#define BH_ABI_VERSION 2
+#define BH_ABI_VERSION 3
 
 typedef struct bh_ctx bh_ctx;
 
@@ -141,17 +141,37 @@ int bh_conv2d_fwd_nchw(bh_ctx *ctx, const float *in, const float *filts, const f
 
 /* Filter-bank transform for the conv variants that read the filters k-major --
  * Boda's xpose_filts (test/rtc/xpose_filts.cucl, run once per var before the
- * timed calls: src/rtc_prof.cc:93-99, src/rtc_fwd.cc:306-326). packed receives
- * bh_conv_filts_packed_floats(OC, IC, KY, KX) floats:
- *  - the k-major bank: row (ky*KX+kx)*IC + ic holds filts[*][ic][ky][kx] for every
- *    output channel (rows padded to a multiple of 4 floats, zero rows up to a
- *    multiple of 64);
- *  - ABI 2: for KY == KX == 3 only, followed by the Winograd F(2x2,3x3) bank U =
- *    G g G^T, [ceil4(IC)][ceil32(OC)][16] floats (each (ic, oc) row's four 4-float
- *    chunks rotated by (oc >> 2) & 3), about 1.8x the k-major bank's size. */
+ * timed calls: src/rtc_prof.cc:93-99, src/rtc_fwd.cc:306-326). A pack is, in order:
+ *  - the k-major bank: row (ky*KX+kx)*IC + ic holds filts[*][ic][ky][kx] for every output
+ *    channel, ceil4(OC) floats per row, ceil64(IC*KY*KX) rows (the padding rows zero);
+ *  - then the Winograd banks its mask names, in bit order (each only for its kernel size):
+ *      BH_BANK_W23  3x3, F(2x2,3x3): U = G g G^T, [ceil4(IC)][ceil32(OC)][16] floats, each
+ *                   (ic, oc) row's four 4-float chunks rotated by (oc >> 2) & 3;
+ *      BH_BANK_W43  3x3, F(4x4,3x3): U = G g G^T over points 0, +-2/3, +-3/2, infinity, made in
+ *                   double and rounded once, [ceil4(IC)][ceil32(OC)][36] floats, the 36
+ *                   positions in the position-split kernels' (group, slot) order;
+ *      BH_BANK_W25  5x5, F(2x2,5x5): the same form and layout as W43 for the 5x5 filter.
+ * bh_conv_filts_pack / bh_conv_filts_packed_floats make the FULL pack (mask BH_BANKS_ALL: a 3x3's
+ * k-major + W23 + W43 = 6.8x the filter bytes, a 5x5's k-major + W25 = 2.4x, other kernels the
+ * k-major bank alone), which bh_conv2d_fwd_nchw_pk / _res / _slab read: any route of the shape
+ * finds its bank there. ABI 3 adds packs of chosen banks: bh_conv_route_banks names the bank the
+ * shape's route reads now (0: none), bh_conv_filts_pack_banks makes a pack of exactly those, and
+ * bh_conv2d_fwd_nchw_pkb takes the mask with the pack. A route whose bank a pack lacks makes it
+ * inside the call (correct, slower). */
+#define BH_BANK_W23 1u
+#define BH_BANK_W43 2u
+#define BH_BANK_W25 4u
+#define BH_BANKS_ALL 0xffffffffu
 size_t bh_conv_filts_packed_floats(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX);
 int bh_conv_filts_pack(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC,
                        uint32_t KY, uint32_t KX);
+size_t bh_conv_filts_packed_floats_banks(uint32_t OC, uint32_t IC, uint32_t KY, uint32_t KX, uint32_t banks);
+int bh_conv_filts_pack_banks(bh_ctx *ctx, const float *filts, float *packed, uint32_t OC, uint32_t IC,
+                             uint32_t KY, uint32_t KX, uint32_t banks);
+/* *banks = the Winograd bank (BH_BANK_*) the route of conv shape dims[0..10] = B,IC,H,W,OC,KY,KX,
+ * sy,sx,py,px reads on ctx now (its tuning table / overrides), 0 for a route of the k-major bank;
+ * ctx may be NULL (the tuning table's / heuristic's route, no device needed) */
+int bh_conv_route_banks(bh_ctx *ctx, const uint32_t *dims, uint32_t *banks);
 /* bh_conv2d_fwd_nchw with the transformed bank of filts already made by
  * bh_conv_filts_pack (packed may be NULL: then a variant that needs it makes it
  * itself, inside the call). filts must still be given: variants that read the
@@ -180,6 +200,14 @@ int bh_conv2d_fwd_nchw_slab(bh_ctx *ctx, const float *in, const float *filts, co
                             uint32_t out_chan_ofs, uint32_t B, uint32_t IC, uint32_t H, uint32_t W,
                             uint32_t OC, uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx,
                             uint32_t py, uint32_t px, int relu);
+/* ABI 3, every conv form in one call: packed (may be NULL) holds the k-major bank + the Winograd
+ * banks of mask `banks` (bh_conv_filts_pack_banks; BH_BANKS_ALL: bh_conv_filts_pack's layout);
+ * res (may be NULL) as _res; the output a channel slab out_chan_ofs .. +OC-1 of a tensor of
+ * out_chans_total channels (0: OC) as _slab (not together with res). */
+int bh_conv2d_fwd_nchw_pkb(bh_ctx *ctx, const float *in, const float *filts, const float *packed, uint32_t banks,
+                           const float *biases, const float *res, float *out, uint32_t out_chans_total,
+                           uint32_t out_chan_ofs, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC,
+                           uint32_t KY, uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu);
 
 /* ---- the other forward layers of Boda's net executor (conv_pipe_fwd_t::gen_op,
  *      src/rtc_fwd.cc:263-405), NCHW fp32 ------------------------------------ */
@@ -241,6 +269,10 @@ int bh_jit_release(bh_ctx *ctx, int module_id);
  * for a shape (op==0: sgemm with dims[0..2] = M,N,K; op==1: conv with
  * dims[0..10] = B,IC,H,W,OC,KY,KX,sy,sx,py,px). */
 int bh_variant_name(int op, const uint32_t *dims, char *buf, size_t buflen);
+/* The same, under ctx's bh_tune_set / bh_tune_set_policy overrides: the variant a call on ctx
+ * runs now. ops-prof names each tune's run by it -- the role of the generated function name
+ * (prc_ret.op->get_func_name(), src/rtc_prof.cc:312) its per-function tolerances key on. */
+int bh_variant_name_ctx(bh_ctx *ctx, int op, const uint32_t *dims, char *buf, size_t buflen);
 
 /* ---- tuning (the backend's counterpart of Boda's op_tune sweeps and wisdom,
  *      src/cnn_op.H:10-31, src/op-tuner.cc). Kernel choice per exact shape comes

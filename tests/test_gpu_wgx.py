@@ -1,13 +1,16 @@
 """Position-split Winograd kernels (bh_wgx.hip, configs wx*) against the oracle.
 
 wx43* is F(4x4, 3x3) and wx23* F(2x2, 3x3) for stride-1 3x3 convs, wx25* F(2x2, 5x5) for stride-1
-5x5 convs (square padding <= R / 2, IC % 4 == 0; the 6x6 forms also IC <= 512). They are forced with
+5x5 convs (square padding <= R / 2, IC % 4 == 0; the 6x6 forms also IC <= 128 / 96). They are forced with
 bh_tune_set on shapes whose 32-tile units run across tile rows and images (outputs that are not a
 multiple of the 4- / 2-wide tile, a last unit only partly filled), ragged output channels (not a
 multiple of the 64- / 128-channel tile, nor of 32), unpadded and non-square inputs. The result is
 an exact-fp32 Winograd sum, checked against the double-accumulated oracle with the tolerances of
-test_gpu_conv.py; the reference widens its own compare to 2e-3 for cuDNN's
-Winograd (src/rtc_prof.cc:314-319), this one does not. A rerun gives the same bits, a pre-packed
+test_gpu_conv.py and, element-wise, with Boda's Winograd tolerance: max
+min_sig_mag_rel_diff(1, ref, out) <= 2e-3, what the reference allows cuDNN's 3x3 Winograd
+(src/rtc_prof.cc:314-319) -- the transforms amplify fp32 cancellation on near-zero outputs, which
+that metric reads as absolute error (points 0, +-2/3, +-3/2 keep the 6x6 forms inside
+it). A rerun gives the same bits, a pre-packed
 bank the same bits as the in-call pack, and the residual / channel-slab epilogues the plain call's
 bits.
 """
@@ -17,7 +20,7 @@ import pytest
 import boda_hip
 from boda_hip import GEN_CONV_BIASES, GEN_CONV_FILTS, GEN_CONV_IN, ops
 from oracle import oracle as orc
-from test_gpu_conv import run_conv
+from test_gpu_conv import WINO_ELEM_TOL, run_conv
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +39,8 @@ SHAPES3 = [
     C(2, 16, 56, 56, 64, 3, 3, 1, 1, 1, 1),    # long tile rows
     C(1, 24, 40, 62, 50, 3, 3, 1, 1, 1, 1),
     C(2, 256, 13, 13, 384, 3, 3, 1, 1, 1, 1),  # a conv-set layer (many stages)
-    C(1, 512, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # IC at the 6x6 forms' limit
+    C(1, 512, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # long K (wx23; over the 6x6 forms' cap)
+    C(1, 128, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # IC at F(4x4,3x3)'s cap
 ]
 SHAPES5 = [
     C(2, 16, 27, 27, 96, 5, 5, 1, 1, 2, 2),    # the AlexNet conv2 geometry, odd output
@@ -45,7 +49,7 @@ SHAPES5 = [
     C(2, 12, 14, 14, 48, 5, 5, 1, 1, 2, 2),
     C(1, 16, 15, 17, 33, 5, 5, 1, 1, 0, 0),    # unpadded, non-square
     C(1, 8, 12, 12, 16, 5, 5, 1, 1, 1, 1),     # pad 1
-    C(2, 96, 27, 27, 256, 5, 5, 1, 1, 2, 2),   # a conv-set layer
+    C(2, 96, 27, 27, 256, 5, 5, 1, 1, 2, 2),   # a conv-set layer, IC at F(2x2,5x5)'s cap
 ]
 
 
@@ -56,8 +60,9 @@ def shapes_of(cn):
 def check(out, s):
     i, f, b = orc.gen_conv(s, 5)
     ref = orc.conv_ref(i, f, b, s, 1)
-    nm, rl2, _ = orc.normalized_errors(ref, out)
+    nm, rl2, hyb = orc.normalized_errors(ref, out)
     assert nm <= 1e-4 and rl2 <= 1e-5, (s, nm, rl2)
+    assert hyb <= WINO_ELEM_TOL, (s, hyb)
 
 
 @pytest.mark.parametrize("cn", WX)
@@ -94,8 +99,8 @@ def test_wx_rejects_other_shapes(dev, cn):
         with pytest.raises(boda_hip.UnsupportedError):  # pad > R / 2
             run_conv(dev, C(1, 16, 28, 28, 16, r, r, 1, 1, r, r))
         if not cn.startswith("wx23"):
-            with pytest.raises(boda_hip.UnsupportedError):  # IC > 512: the 6x6 forms' fp32 error
-                run_conv(dev, C(1, 516, 14, 14, 16, r, r, 1, 1, 1, 1))
+            with pytest.raises(boda_hip.UnsupportedError):  # IC over the 6x6 forms' cap (element error)
+                run_conv(dev, C(1, 132 if r == 3 else 100, 14, 14, 16, r, r, 1, 1, 1, 1))
     finally:
         dev.tune_set(1, -1, 0)
 

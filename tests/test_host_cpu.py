@@ -38,7 +38,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(boda_hip.LIB_PATH)
     for s in header_symbols():
         assert hasattr(lib, s), s
-    assert boda_hip.lib().bh_abi_version() == 2
+    assert boda_hip.lib().bh_abi_version() == 3
 
 
 def test_library_is_gfx950_code_object():

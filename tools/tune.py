@@ -51,6 +51,35 @@ def bk_of(name):
 
 FLUSH = None
 
+# Winograd candidates are admitted only inside Boda's Winograd tolerance: the element-wise
+# min_sig_mag_rel_diff(1, ., .) against the double-accumulated oracle <= WINO_TOL, the reference's
+# widening for cuDNN's 3x3 Winograd (src/rtc_prof.cc:314-319). Checked on up to GATE_SAMPLES
+# outputs (all of them for smaller ops); tests/test_gpu_*.py assert it on the full tensors.
+WINO_TOL = 2e-3
+GATE_SAMPLES = 1 << 17
+_REF = {}
+
+
+def wino_error(wl, s, i=0):
+    """Max element metric of op i's current output (the route just run) against the oracle."""
+    import numpy as np
+    from oracle import oracle as orc
+    key = tuple(s.as_dims())
+    if key not in _REF:
+        inp, filts, biases = orc.gen_conv(s, 5)
+        n = s.B * s.OC * s.OH * s.OW
+        if n <= GATE_SAMPLES:
+            _REF[key] = (None, orc.conv_ref(inp, filts, biases, s, 1))
+        else:
+            idx = np.random.default_rng(5).choice(n, GATE_SAMPLES, replace=False).astype(np.uint64)
+            _REF[key] = (idx.astype(np.int64), orc.conv_ref_at(inp, filts, biases, s, idx, 1))
+    idx, ref = _REF[key]
+    wl.launch(i)
+    got = wl.output(i)
+    if idx is not None:
+        got = got[idx]
+    return orc.normalized_errors(ref, got)[2]
+
 
 TIMING = "graph"
 
@@ -228,12 +257,19 @@ def main():
                 cand = []
             if key in prev and prev[key][0] in names[kind]:
                 cand.append((names[kind].index(prev[key][0]), prev[key][1]))
+            rejected = set()
             for ci, S in cand:
                 dev.tune_set(kind, ci, S)
                 try:
                     t = time_op(dev, wl, 0, args.reps)
                 except boda_hip.UnsupportedError:
                     continue
+                if names[kind][ci].startswith(("wg", "wx")):
+                    err = wino_error(wl, s)
+                    if err > WINO_TOL:  # outside the Winograd tolerance: never routed
+                        results.append({"key": key, "cfg": names[kind][ci], "splits": S, "ms": t, "rejected": err})
+                        rejected.add((names[kind][ci], S))
+                        continue
                 results.append({"key": key, "cfg": names[kind][ci], "splits": S, "ms": t})
                 if t > 5.0:  # long ops: a progress line per candidate (a silent minute reads as a hang)
                     print("   %s S=%+d %.4f ms" % (names[kind][ci], S, t), flush=True)
@@ -243,17 +279,21 @@ def main():
             results.append({"key": key, "cfg": "default", "splits": 0, "ms": t_def})
             if args.confirm > 0:
                 # the TOP routes of the sweep and the table's choice, timed again: medians decide
-                mine = sorted([x for x in results if x["key"] == key and x["cfg"] != "default" and "wt" not in x],
-                              key=lambda x: x["ms"])
+                mine = sorted([x for x in results if x["key"] == key and x["cfg"] != "default" and "wt" not in x
+                               and "rejected" not in x], key=lambda x: x["ms"])
                 fin, seen = [], set()
                 for x in mine:
                     k2 = (x["cfg"], x["splits"])
                     if k2 not in seen and len(fin) < args.top:
                         seen.add(k2)
                         fin.append(k2)
-                if key in prev and prev[key] not in seen and prev[key][0] in names[kind]:
+                if (key in prev and prev[key] not in seen and prev[key][0] in names[kind]
+                        and prev[key] not in rejected):
                     fin.append(prev[key])
-                med = {}
+                # the default route (table off: the heuristic) competes too, so a confirmed route
+                # slower than it is never written
+                dev.tune_set(kind, -1, 0)
+                med = {("default", 0): statistics.median(time_op(dev, wl, 0, args.reps) for _ in range(args.confirm))}
                 for cn, S in fin:
                     dev.tune_set(kind, names[kind].index(cn), S)
                     try:
@@ -263,12 +303,11 @@ def main():
                 dev.tune_set(kind, -1, 0)
                 for (cn, S), t in med.items():
                     results.append({"key": key, "cfg": cn, "splits": S, "ms": t, "confirm": args.confirm})
-                if med:
-                    (cn, S), t = min(med.items(), key=lambda kv: kv[1])
-                    best = (t, names[kind].index(cn), S)
-                    if key in prev and prev[key] in med and t >= (1 - args.min_gain) * med[prev[key]]:
-                        best = (med[prev[key]], names[kind].index(prev[key][0]), prev[key][1])
-            elif key in prev:  # keep the table's choice unless clearly beaten in this run
+                (cn, S), t = min(med.items(), key=lambda kv: kv[1])
+                best = (t, -1, 0) if cn == "default" else (t, names[kind].index(cn), S)
+                if key in prev and prev[key] in med and t >= (1 - args.min_gain) * med[prev[key]]:
+                    best = (med[prev[key]], names[kind].index(prev[key][0]), prev[key][1])
+            elif key in prev and prev[key] not in rejected:  # keep the table's choice unless clearly beaten
                 pt = [x["ms"] for x in results if x["key"] == key and x["cfg"] == prev[key][0]
                       and x["splits"] == prev[key][1]]
                 if pt and best[0] >= (1 - args.min_gain) * pt[0]:
