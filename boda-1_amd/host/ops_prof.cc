@@ -173,7 +173,7 @@ int main(int argc, char **argv) {
                    "  [--op-tunes='(tag=(use_be=hip,cfg=NAME,splits=N,wt=W),...)'] [--kg-tune-tag=tag]\n"
                    "  [--func-mrd-toler='(variant-or-word=toler,...)'] [--wino-mrd-toler=2e-3] [--max-err=10]\n"
                    "  [--gen-data-mode=5] [--run-iter=1] [--mrd-toler=2e-4] [--device=0] [--write-runs=0]\n"
-                   "  [--write-kg-digest=1]\n"
+                   "  [--write-kg-digest=1] [--live-mrd-toler=0]\n"
                    "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F | --list-shard=k/n --ops-fn=F\n";
       return 2;
     }
@@ -216,6 +216,11 @@ int main(int argc, char **argv) {
     // Winograd routes widen to 2e-3, the reference's widening for cuDNN's 3x3 Winograd
     // (src/rtc_prof.cc:314-319), unless --func-mrd-toler names them
     const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-3"));
+    // --live-mrd-toler (MI355X extension, default 0: the reference's single tolerance): a floor for
+    // the full-data compare only, the digest compare keeps the function's tolerance. Two fp32
+    // routes summing K in different orders differ element-wise by about their error against the
+    // exact sum, far above a digest's 2e-4 at K in the thousands
+    const double live_floor = std::stod(o.get("live-mrd-toler", "0"));
     auto toler_of = [&](std::string const &variant) {
       double t = mrd;
       size_t best = 0;
@@ -350,7 +355,7 @@ int main(int argc, char **argv) {
         std::string dstat = "n/a", cstat = "n/a";
         double worst_mrd = 0;
         if (err.str().empty()) {
-          const double vmt = toler_of(variant);
+          const double vmt = toler_of(variant), lvmt = std::max(vmt, live_floor);
           if (have_kg) {  // full-data compare against the known-good run
             cstat = "ok";
             for (auto const &kv : vs_kg) {
@@ -358,7 +363,7 @@ int main(int argc, char **argv) {
               if (it == outs.end()) rt_err("reg/comp out var set mismatch for tune " + tag);
               double m = 0;
               std::ostringstream cv;
-              if (comp_var(cv, kv.first, kv.second->dims, *kv.second->data, *it->second->data, vmt, max_err, &m)) {
+              if (comp_var(cv, kv.first, kv.second->dims, *kv.second->data, *it->second->data, lvmt, max_err, &m)) {
                 ++num_mad_fail;
                 cstat = "FAIL";
                 err << cv.str();
@@ -392,10 +397,10 @@ int main(int argc, char **argv) {
           char buf[640];
           std::snprintf(buf, sizeof(buf),
                         "op_ix=%zu tune=%s func=%s secs=%.6e gflops=%.1f roofline=%.1f%% mrd_vs_kg=%.3e toler=%.1e "
-                        "comp=%s digest=%s\n",
+                        "comp=%s dtoler=%.1e digest=%s\n",
                         ix, tag.c_str(), variant.empty() ? op.func_name.c_str() : variant.c_str(), run.rt_secs,
-                        w.flops / run.rt_secs / 1e9, 100.0 * roofline_secs(w) / run.rt_secs, worst_mrd, vmt,
-                        cstat.c_str(), dstat.c_str());
+                        w.flops / run.rt_secs / 1e9, 100.0 * roofline_secs(w) / run.rt_secs, worst_mrd, lvmt,
+                        cstat.c_str(), vmt, dstat.c_str());
           *out << buf;
         }
         run.err = err.str();

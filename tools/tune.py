@@ -53,10 +53,13 @@ FLUSH = None
 
 # Winograd candidates are admitted only inside Boda's Winograd tolerance: the element-wise
 # min_sig_mag_rel_diff(1, ., .) against the double-accumulated oracle <= WINO_TOL, the reference's
-# widening for cuDNN's 3x3 Winograd (src/rtc_prof.cc:314-319). Checked on up to GATE_SAMPLES
-# outputs (all of them for smaller ops); tests/test_gpu_*.py assert it on the full tensors.
+# widening for cuDNN's 3x3 Winograd (src/rtc_prof.cc:314-319). Checked on the whole output up to
+# GATE_FULL_FLOPS (as tests/test_gpu_routed.py checks it), above that on GATE_SAMPLES outputs at
+# GATE_MARGIN of the tolerance (a sample's maximum understates the tensor's).
 WINO_TOL = 2e-3
-GATE_SAMPLES = 1 << 17
+GATE_FULL_FLOPS = 2e10
+GATE_SAMPLES = 1 << 18
+GATE_MARGIN = 0.8
 _REF = {}
 
 
@@ -68,7 +71,7 @@ def wino_error(wl, s, i=0):
     if key not in _REF:
         inp, filts, biases = orc.gen_conv(s, 5)
         n = s.B * s.OC * s.OH * s.OW
-        if n <= GATE_SAMPLES:
+        if n <= GATE_SAMPLES or s.flops() <= GATE_FULL_FLOPS:
             _REF[key] = (None, orc.conv_ref(inp, filts, biases, s, 1))
         else:
             idx = np.random.default_rng(5).choice(n, GATE_SAMPLES, replace=False).astype(np.uint64)
@@ -78,7 +81,7 @@ def wino_error(wl, s, i=0):
     got = wl.output(i)
     if idx is not None:
         got = got[idx]
-    return orc.normalized_errors(ref, got)[2]
+    return orc.normalized_errors(ref, got)[2] / (1.0 if idx is None else GATE_MARGIN)
 
 
 TIMING = "graph"
