@@ -434,6 +434,274 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 #endif
 }
 
+// Resident-weight form (configs dc<k>s<s>r*, round 5). PMC of the b20 11x11 s4 stem on dc_kernel
+// (profiles/r04/pmc_stems.json): the MFMA pipe 65 % busy, 64 % of wave cycles waiting on the stage
+// ring, ~38 KB of LDS-DMA per 61-step stage (the weights [2 KK2][OCT] re-fetched for every tile and
+// channel: 43 % of it) -- about 8.7 B/clk per CU at two blocks per CU, above what the LDS-DMA path
+// sustains. Here a block of NW = 8 waves owns ONE OC tile for its whole life (a grid that is a
+// multiple of the OC tiles, tiles dealt OC-fastest), so:
+//  * every input channel's weights [2 KK2 taps][OCT] and the tile's biases are DMA'd into LDS once,
+//    in the prologue (IC <= ICMAX), and stay resident;
+//  * the ring carries only the input strips: one per (tile, input channel) stage, RIN rows of the
+//    NPX = 32 NW pixels' input at pitch WPM -- 256 pixels' rows, which overlap, for what two
+//    128-pixel blocks fetched twice;
+//  * a step is as in dc_kernel: A = resident weights (one ds_read_b32 per tile), B = the strip at a
+//    compile-time tap offset from one of three per-lane bases; the next stage's strip DMAs spread
+//    over the first IS steps, the previous tile's output stores deferred into the first steps.
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX>
+__global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
+  constexpr int NT = NW * 64, NPX = NW * 32, OCT = 32 * TM;
+  constexpr int KK = KY * KX, KK2 = (KK + 1) / 2;
+  constexpr int WPC = 2 * KK2 * OCT / 4;                    // 16-B weight pieces per input channel
+  constexpr int LWA = (WPC + NT - 1) / NT;                  // weight DMA instructions per wave and channel
+  constexpr int WREGC = LWA * NT * 4;                       // floats per channel (whole DMA instructions)
+  constexpr int BREG = ((OCT + 63) / 64) * 64;              // biases: one dword DMA per 64 channels
+  constexpr int SF = RIN * WPM;
+  constexpr int PW = V4 ? 4 : 1;
+  static_assert(WPM % PW == 0, "16-B strip rows");
+  constexpr int LWB = (SF / PW + NT - 1) / NT;              // strip DMA instructions per wave and stage
+  constexpr int SREG = LWB * NT * PW;                       // floats per strip slot
+  static_assert(D >= 2 && (D - 2) * LWB <= 63, "vmcnt range");
+  static_assert(OCT % 4 == 0 && BREG <= NT, "16-B weight pieces, one bias DMA per wave at most");
+  constexpr int PF = TM >= 2 ? 2 : 3;                       // LDS fragment prefetch distance (steps)
+  constexpr int IS = (KK2 + 1) / 2 > 1 ? (KK2 + 1) / 2 : 1;   // steps the next stage's DMAs are spread over
+  constexpr int NST = TM * 4;                               // deferred float4 stores per lane and tile
+  constexpr int ISS = KK2 > 2 * NST ? 2 * NST : KK2;
+  // one __shared__ array: [ICMAX channels' weights][biases][D strip slots]
+  __shared__ __attribute__((aligned(16))) float smem[ICMAX * WREGC + BREG + D * SREG];
+  float *const wres = smem, *const bres = smem + ICMAX * WREGC, *const ring = bres + BREG;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = lane >> 5, li = lane & 31;
+  KT(0);
+
+  // ---- this block's OC tile (fixed: gridDim.x is a multiple of the OC tiles, p.ipt) and its tiles
+  // t = blockIdx.x + i * gridDim.x = (pixel run, image, OC tile), OC tile fastest
+  const uint32_t G = gridDim.x, b0 = blockIdx.x;
+  const uint32_t ntile = p.total_it;
+  const uint32_t my_tiles = b0 < ntile ? (ntile - b0 + G - 1) / G : 0;
+  const uint32_t oc0 = (b0 - fdiv(b0, p.ipt_m, p.ipt_s) * p.ipt) * OCT;
+  auto decode = [&](uint32_t t, uint32_t &img, uint32_t &p0) {
+    const uint32_t rest = fdiv(t, p.ipt_m, p.ipt_s);
+    img = fdiv(rest, p.tm_m, p.tm_s);
+    p0 = (rest - img * p.tiles_n) * NPX;
+  };
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsi = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+
+  // ---- resident weights and biases: piece e of channel ic's [tap][OCT] image is packed-bank row
+  // tap * IC + ic (K order (ky, kx, ic)), columns oc0 + 4 (e % (OCT / 4)); taps >= KK (the odd
+  // kernel's padding tap) and columns past OC4 miss: zeros
+#pragma unroll
+  for (int j = 0; j < LWA; ++j) {
+    const uint32_t e = (uint32_t)((j * NW + wave) * 64 + lane), tap = e / (OCT / 4), c4 = 4 * (e % (OCT / 4));
+    const uint32_t off = oob_unless((tap < (uint32_t)KK) & (oc0 + c4 < p.lda), (tap * p.IC * p.lda + oc0 + c4) * 4u);
+    for (uint32_t ic = 0; ic < p.IC; ++ic) dma16s(rsw, wres + ic * WREGC + (j * NW + wave) * 256, off, ic * p.lda * 4u);
+  }
+  if (64 * wave < BREG)
+    dma4(rsbias, bres + 64 * wave, oob_unless(oc0 + 64 * wave + lane < p.M, (oc0 + 64 * wave + lane) * 4u));
+
+  // ---- strip DMA sources: element e = (row r, column c) of the [RIN][WPM] image; per tile the lane
+  // part (tvo, VGPRs), per channel the scalar soffset ic * HW; dead stages (past the block's last
+  // tile) miss, so every wave always has the same DMAs in flight
+  const uint32_t pxa = V4 ? (p.px ? 4u : 0u) : p.px;  // strip column of input x = 0
+  uint32_t srel[LWB], srow[LWB], tvo[LWB];
+#pragma unroll
+  for (int j = 0; j < LWB; ++j) {
+    const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane) * PW;
+    const uint32_t r = e / WPM, c = e - r * WPM;
+    const int x = (int)c - (int)pxa;
+    srow[j] = ((r < (uint32_t)RIN) & ((uint32_t)x < p.W)) ? r : 0xffffu;
+    srel[j] = (r * p.W + (uint32_t)x) * 4u;
+  }
+  auto plan_tile = [&](uint32_t i) {
+    uint32_t img, p0;
+    decode(b0 + i * G, img, p0);
+    const uint32_t dead = i < my_tiles ? 0u : OOB;
+    const int ya = (int)(fdiv(p0, p.ow_m, p.ow_s) * S) - (int)p.py;  // input row of strip row 0
+    const uint32_t rlo = (uint32_t)max(0, -ya), rhi = (uint32_t)max(0, (int)p.H - ya);
+    const uint32_t sb = img * p.ICHW * 4u + (uint32_t)(ya * (int)p.W) * 4u;
+#pragma unroll
+    for (int j = 0; j < LWB; ++j) tvo[j] = oob_unless((srow[j] >= rlo) & (srow[j] < rhi), srel[j] + sb) | dead;
+  };
+  auto issue_one = [&](int q, int slot, uint32_t ic) {
+    float *const base = ring + slot * SREG + (wave * LWB + q) * 64 * PW;
+    if constexpr (V4) dma16s(rsi, base, tvo[q], ic * p.HW * 4u);
+    else dma4s(rsi, base, tvo[q], ic * p.HW * 4u);
+  };
+
+  f32x16 acc[TM];
+  uint32_t poff = 0;  // this lane's pixel's strip offset in the current tile (bytes)
+  uint32_t hsel = kh ? 0xffffffffu : 0u;
+  f32x4v dval[NST];
+  uint32_t dbase[TM], dpx = 0, dhw = 0;
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  auto store_one = [&](int q) {  // deferred float4 piece q = (t, gq) of the previous tile
+    const int t = q / 4, gq = q % 4;
+    const uint32_t px = dpx + (uint32_t)(8 * gq);
+    const uint32_t off = dbase[t] + (uint32_t)(8 * gq) * 4u;
+    if (px + 4 <= dhw) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
+                                             rso, off, 0, AUX_OUT);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = dval[q][e];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, xe), rso,
+                                              oob_unless(px + (uint32_t)e < dhw, off + 4u * (uint32_t)e), 0, AUX_OUT);
+      }
+    }
+  };
+
+  // one stage = one input channel of one tile (KK2 steps of TM MFMAs); stage g_issue's strip DMAs
+  // go out over the first IS steps, the previous tile's deferred stores over the first ISS
+  auto compute = [&](int slot, int islot, uint32_t ic, uint32_t g_issue, bool dstores) {
+    const uint32_t i_issue = fdiv(g_issue, p.ic_m, p.ic_s), ic_issue = g_issue - i_issue * p.IC;
+    if (ic_issue == 0) plan_tile(i_issue);  // wave-uniform
+    const float *const Ab = wres + ic * WREGC + kh * KK2 * OCT + li;
+    const char *const Sb = (const char *)(ring + slot * SREG);
+    // lane half 1 reads tap KK2 + s where half 0 reads tap s: three per-lane bases (dc_kernel)
+    constexpr int CSH = KK2 % KX, RSH = KK2 / KX;
+    constexpr int DLO = RSH * WPM + CSH, DHI = (RSH + 1) * WPM + CSH - KX;
+    constexpr int DPAD = -dc_koff<KX, WPM>(KK2 - 1, KK);
+    asm volatile("" : "+v"(hsel));
+    const char *bs[3] = {Sb + poff + (hsel & (uint32_t)(DLO * 4)), Sb + poff + (hsel & (uint32_t)(DHI * 4)),
+                         Sb + poff + (int)(hsel & (uint32_t)(DPAD * 4))};
+    auto frag = [&](int s, float (&a)[TM], float &b) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a[t] = Ab[s * OCT + 32 * t];
+      const int k0 = dc_koff<KX, WPM>(s, KK) * 4;
+      const int kind = KK2 + s >= KK ? 2 : (s % KX < KX - CSH ? 0 : 1);
+      b = *(const float *)(bs[kind] + k0);
+    };
+    float a[PF + 1][TM], b[PF + 1];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) frag(s, a[s], b[s]);
+#pragma unroll
+    for (int s = 0; s < KK2; ++s) {
+      if (s + PF < KK2) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)], a[s % (PF + 1)][t], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int q = (s * LWB + IS - 1) / IS; q < ((s + 1) * LWB + IS - 1) / IS && q < LWB; ++q) issue_one(q, islot, ic_issue);
+      if (dstores) {
+#pragma unroll
+        for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- prologue: strips of stages 0 .. D-2 (behind the resident weights: the first stage's wait
+  // covers them)
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) {
+    const uint32_t i_s = fdiv((uint32_t)s, p.ic_m, p.ic_s), ic_s = (uint32_t)s - i_s * p.IC;
+    if (ic_s == 0) plan_tile(i_s);
+#pragma unroll
+    for (int q = 0; q < LWB; ++q) issue_one(q, s, ic_s);
+  }
+  const bool vec = !p.res;
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  bool pending = false;
+  int slot = 0;
+  uint32_t g = 0;
+  for (uint32_t i = 0; i < my_tiles; ++i) {
+    uint32_t img, p0;
+    decode(b0 + i * G, img, p0);
+    const uint32_t oy_a = fdiv(p0, p.ow_m, p.ow_s);
+    {
+      const uint32_t px = p0 + (uint32_t)(wave * 32 + li);
+      const uint32_t oy = fdiv(px, p.ow_m, p.ow_s), ox = px - oy * p.OW;
+      poff = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S + pxa - p.px) * 4u : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    for (uint32_t ic = 0; ic < p.IC; ++ic, ++g) {
+      vm_wait<(D - 2) * LWB>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage g (and, the first time, the weights) landed; all done with g-1
+      asm volatile("" ::: "memory");
+      if (i == 0 && ic == 0) KT(1);
+      compute(slot, slot == 0 ? D - 1 : slot - 1, ic, g + D - 1, pending);
+      pending = false;
+      slot = slot == D - 1 ? 0 : slot + 1;
+    }
+    if (i == 0) KT(2);
+    // ---- epilogue: acc[t][4 gq + e] is output channel oc0 + 32 t + li, pixel p0 + 32 wave + 8 gq +
+    // 4 kh + e: bias, ReLU, 16-B pieces deferred into the next tile's first steps (stored now after
+    // the block's last tile); with a residual, element stores now
+    const uint32_t obase = img * p.OCOHW;
+    if (vec) {
+      dpx = p0 + (uint32_t)(wave * 32 + 4 * kh);
+      dhw = p.OHW;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const uint32_t m = oc0 + 32 * t + li;
+        const float bb = bres[32 * t + li];
+        dbase[t] = oob_unless(m < p.M, (obase + m * p.OHW + dpx) * 4u);
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          f32x4v v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = acc[t][4 * gq + e] + bb;
+            v[e] = (p.relu && x < 0.0f) ? 0.0f : x;
+          }
+          dval[t * 4 + gq] = v;
+        }
+      }
+      if (i + 1 < my_tiles) {
+        pending = true;
+      } else {
+#pragma unroll
+        for (int q = 0; q < NST; ++q) store_one(q);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const uint32_t m = oc0 + 32 * t + li;
+        const float bb = bres[32 * t + li];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t px = p0 + (uint32_t)(wave * 32 + 8 * (r >> 2) + 4 * kh + (r & 3));
+          const uint32_t o = oob_unless((m < p.M) & (px < p.OHW), (obase + m * p.OHW + px) * 4u);
+          float x = acc[t][r] + bb;
+          if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
+          x = (p.relu && x < 0.0f) ? 0.0f : x;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, AUX_OUT);
+        }
+      }
+    }
+    if (i == 0) KT(3);
+  }
+  vm_wait<0>();
+#ifdef BH_KTRACE
+  KT(4);
+#endif
+}
+
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX>
+cfg_t dcr_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * NW, 2 * ((KY * KX + 1) / 2), 64 * NW, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = dcr_kernel<KY, KX, S, WPM, RIN, TM, NW, D, V4, ICMAX>;
+  c.dc_ci = V4;
+  c.dc = 1;
+  c.dc_ky = KY;
+  c.dc_kx = KX;
+  c.dc_s = S;
+  c.dc_wpm = WPM;
+  c.dc_rin = RIN;
+  c.dc_icmax = ICMAX;  // resident weights: input channels <= ICMAX, grid a multiple of the OC tiles
+  return c;
+}
+
 template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0>
 cfg_t dc_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 128 * TN, 2 * ((KY * KX + 1) / 2), 256, {}, 1};
@@ -481,6 +749,16 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<6, 6, 2, 516, 10, 2, 2, 2, 1>("dc6s2x64n256w516d2v"),
       dc_cfg<11, 11, 2, 228, 15, 1, 1, 2, 1>("dc11s2x32d2v"),
       dc_cfg<11, 11, 2, 228, 15, 3, 1, 2, 1>("dc11s2x96d2v"),
+      // resident weights, 8 waves x 32 pixels, one OC tile per block (round 5)
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3>("dc11s4r32d2"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 3, 0, 3>("dc11s4r32d3"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 1, 3>("dc11s4r32d2v"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 3, 1, 3>("dc11s4r32d3v"),
+      dcr_cfg<7, 7, 2, 236, 13, 2, 8, 2, 0, 3>("dc7s2r64d2"),
+      dcr_cfg<7, 7, 2, 236, 13, 2, 8, 3, 0, 3>("dc7s2r64d3"),
+      dcr_cfg<7, 7, 2, 236, 13, 2, 8, 2, 1, 3>("dc7s2r64d2v"),
+      dcr_cfg<7, 7, 2, 236, 13, 2, 8, 3, 1, 3>("dc7s2r64d3v"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3>("dc7s2r32d3v"),
       // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
       dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
       dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),
@@ -515,12 +793,17 @@ int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY,
   const uint32_t octiles = (p.M + c.BM - 1) / c.BM;
   const uint64_t ntile = (uint64_t)B * tiles * octiles;
   if (ntile >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: too many tiles");
-  // persistent grid: as many blocks as fit on the device at once (each loops over tiles)
+  if (c.dc_icmax && p.IC > (uint32_t)c.dc_icmax)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " keeps at most " + std::to_string(c.dc_icmax) +
+                                  " input channels' weights resident");
+  // persistent grid: as many blocks as fit on the device at once (each loops over tiles); the
+  // resident-weight form: a multiple of the OC tiles, so that every block keeps one OC tile
   const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
   int bpc = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k, 256, 0) != hipSuccess || bpc < 1) bpc = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k, c.NT, 0) != hipSuccess || bpc < 1) bpc = 1;
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
-  const uint32_t G = (uint32_t)std::min<uint64_t>(ntile, (uint64_t)ncu * std::min(bpc, 4));
+  uint32_t G = (uint32_t)std::min<uint64_t>(ntile, (uint64_t)ncu * std::min(bpc, 4));
+  if (c.dc_icmax) G = std::max(octiles, G / octiles * octiles);
   p.total_it = (uint32_t)ntile;
   p.tiles_n = tiles;
   p.ipt = octiles;
@@ -537,7 +820,7 @@ int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY,
   p.trace = (unsigned long long *)ctx->stamps + 65536;
 #endif
   void *args[] = {&p};
-  return bh::launch(ctx, k, dim3(G, 1, 1), dim3(256), args, first, true, "conv_direct");
+  return bh::launch(ctx, k, dim3(G, 1, 1), dim3(c.NT), args, first, true, "conv_direct");
 }
 
 }  // namespace bhk

@@ -356,6 +356,7 @@ struct cfg_t {
   int streamk = 0;    // persistent stream-K grid (srk_kernel): k[..][..][0] only
   int lds_bytes = 0;  // static LDS per block (stream-K grid sizing)
   int gv = 0;         // filter-streaming kernel (bh_gv.hip): grid (M / BM) x K chunks, BN >= N
+  int dc_icmax = 0;   // dc == 1 resident-weight form: input channels it keeps resident (0: the ring form)
   int dc = 0;         // direct conv (bh_direct.hip; 2: bh_dcm.hip, 3: bh_k1s.hip): kernel dc_ky x dc_kx, stride dc_s, strip dc_rin x dc_wpm
   int dc_ky = 0, dc_kx = 0, dc_s = 0, dc_wpm = 0, dc_rin = 0;
   int dc_ci = 0;      // dc == 2 (bh_dcm.hip): input channels per stage
