@@ -754,6 +754,7 @@ cfg_t sgemm_cfg(const char *name) {
 // Tile configurations (BM x BN x BK; 32x32 MFMA tiles per wave TM x TN; waves M x N).
 std::vector<cfg_t> with_ring(int op, std::vector<cfg_t> v) {
   for (auto const &c : ring_cfgs(op)) v.push_back(c);
+  for (auto const &c : ref64_cfgs()) v.push_back(c);
   if (op == 1) {
     for (auto const &c : gv_cfgs()) v.push_back(c);
     for (auto const &c : dc_cfgs()) v.push_back(c);
@@ -1070,6 +1071,7 @@ std::string describe_cfg(int op, const uint32_t *d, choice_t const &ch) {
   cfg_t const &c = cfgs(op)[ch.cfg];
   uint32_t M, N, K;
   std::string s;
+  if (c.ref64) return std::string(op == 0 ? "ref64_sgemm" : "ref64_conv") + "_double";
   if (op == 0) {
     M = d[0]; N = d[1]; K = d[2];
     s = std::string("mfma32_sgemm_") + c.name + ((M % 4 == 0 && N % 4 == 0) ? "_vec" : "_scalar");
@@ -1158,6 +1160,7 @@ int launch_sgemm(bh_ctx *ctx, const float *a, const float *b, float *c, uint32_t
   p.wt = ch.wt && fits_buffer((uint64_t)M * N * 4);
   if (getenv("BH_EXP_RING_DWORD_B") && vec && cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0])  // experiment
     return launch_gemm(ctx, 0, ch, A_KSCALAR, B_KSCALAR, p, "sgemm");
+  if (cfgs(0)[ch.cfg].ref64) return launch_ref64_sgemm(ctx, p);
   if (!vec && (!cfgs(0)[ch.cfg].k[A_KSCALAR][B_KSCALAR][0] || cfgs(0)[ch.cfg].name[0] == 'r')) ch = heuristic(0, d, false);
   return launch_gemm(ctx, 0, ch, vec ? A_KVEC : A_KSCALAR, vec ? B_KVEC : B_KSCALAR, p, "sgemm");
 }
@@ -1203,6 +1206,10 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
   p.wt = ch.wt;  // the output fits a 2 GiB buffer (checked above)
   if (no_dc && cfgs(1)[ch.cfg].dc) ch = heuristic(1, d, true, false);
   const bool first = !repacked;
+  if (cfgs(1)[ch.cfg].ref64) {  // the double-accumulating known-good kernel (reference layouts)
+    p.IC = IC;
+    return launch_ref64_conv(ctx, p, B, KY, first);
+  }
   if (cfgs(1)[ch.cfg].gv && !cfgs(1)[ch.cfg].packA) {
     // few output columns: stream the bank in its reference layout; the window covering the
     // whole unpadded input makes the im2col the input itself (B_FC, 16-B loads). Shape

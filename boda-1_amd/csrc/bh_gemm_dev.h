@@ -362,6 +362,7 @@ struct cfg_t {
   int dc_ci = 0;      // dc == 2 (bh_dcm.hip): input channels per stage
   int gv_cx = 1;      // gv: interleaved column tiles (1x1, a lane's gv_cx pixels per load)
   int fcv = 0;        // gv: batch-streaming ipconv kernel (bh_gv.hip fcv_kernel), batch <= BN
+  int ref64 = 0;      // double-accumulating known-good kernel (bh_ref64.hip), never tuned in
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and
@@ -371,6 +372,10 @@ std::vector<cfg_t> ring_cfgs(int op);
 std::vector<cfg_t> gv_cfgs();
 // bh_direct.hip: direct-conv configurations for the few-channel stem layers
 std::vector<cfg_t> dc_cfgs();
+// bh_ref64.hip: the double-accumulating known-good configuration "ref64" of conv and SGEMM
+std::vector<cfg_t> ref64_cfgs();
+int launch_ref64_conv(bh_ctx *ctx, GemmArgs &p, uint32_t B, uint32_t KY, bool first);
+int launch_ref64_sgemm(bh_ctx *ctx, GemmArgs &p);
 int launch_dc(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
               uint32_t sx, bool first);
 // bh_dcm.hip: multi-channel direct-conv configurations for stride-1 3x3 / 5x5 convs

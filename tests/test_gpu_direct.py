@@ -38,7 +38,8 @@ SHAPES = {
               ops.ConvShape(1, 4, 120, 100, 100, 11, 11, 4, 4, 5, 5),
               ops.ConvShape(1, 4, 100, 224, 40, 11, 11, 4, 4, 1, 1),  # W % 4 == 0, pad 1 (16-B strip)
               ops.ConvShape(1, 3, 100, 516, 96, 11, 11, 4, 4, 0, 0),  # op_sigs' 516-wide stem rows
-              ops.ConvShape(2, 2, 60, 300, 20, 11, 11, 4, 4, 2, 2)],
+              ops.ConvShape(2, 2, 60, 300, 20, 11, 11, 4, 4, 2, 2),
+              ops.ConvShape(2, 3, 64, 128, 40, 11, 11, 4, 4, 2, 2)],  # W % 4 == 0, IC 3: resident-weight 16-B strips
     (6, 2): [ops.ConvShape(1, 3, 100, 516, 40, 6, 6, 2, 2, 0, 0),    # op_sigs' 516-wide 6x6 s2 stem rows
              ops.ConvShape(2, 2, 64, 132, 20, 6, 6, 2, 2, 1, 1),     # 3-row pixel tiles, pad 1
              ops.ConvShape(1, 4, 40, 60, 33, 6, 6, 2, 2, 0, 2),

@@ -71,10 +71,10 @@ def test_ops_prof_all_is_well(suite, ops_fn, mode, nops, tmp_path):
 # ops-prof's multi-tune sweep (src/rtc_prof.cc:276-345; the reference's own invocation,
 # test/test_cmds.xml:110: --op-tunes with a kg tune, --kg-tune-tag, --func-mrd-toler): every tune
 # of every op is compared element-wise with the known-good tune's full output, and its digest with
-# the stored known-good digest. The kg tune is the most accurate route on these lists, the
-# register-streaming kernel that sums K in chunks (at most 4.6e-4 from float64 over the 3x3 list,
-# profiles/r05/route_acc_3x3.txt); the others are the tuning table's route, the generic im2col tile
-# kernel, a multi-channel direct conv and F(4x4,3x3) /
+# the stored known-good digest. The kg tune is "ref64", the double-accumulating known-good kernel
+# (bh_ref64.hip: an exact sum rounded once), so each compare measures the tune's own error; the
+# others are the tuning table's route, the generic im2col tile kernel, a multi-channel direct conv,
+# the K-chunked register-streaming kernel and F(4x4,3x3) /
 # F(2x2,3x3) / F(2x2,5x5) Winograd forms (UNSUP on the shapes a form does not serve: recorded as a
 # profile call failure, as the reference records unsup_err, not a MAD failure).
 # Tolerance: the digests compare at the reference's 2e-4 (2e-3 for Winograd variants, :314-319).
@@ -85,7 +85,7 @@ def test_ops_prof_all_is_well(suite, ops_fn, mode, nops, tmp_path):
 # kernel 7.3e-4, the K-chunked register-streaming kernel 4.6e-4). The reference widened its own
 # cross-implementation compare to 4e-4 (cuDNN, test_cmds.xml:110) for kernels that sum in the same
 # order; an element-wise 2e-4 across summation orders is not attainable in fp32.
-TUNES = ("(kg=(use_be=hip,cfg=gvs64x32w8),tab=(use_be=hip),dm=(cfg=dm3w16x64c8),tile=(cfg=128x128x32),"
+TUNES = ("(kg=(use_be=hip,cfg=ref64),tab=(use_be=hip),dm=(cfg=dm3w16x64c8),tile=(cfg=128x128x32),gvs=(cfg=gvs64x32w8),"
          "wx43=(cfg=wx43s12),wx23=(cfg=wx23s6),wx25=(cfg=wx25s6),wgi=(cfg=wgi128x32))")
 MULTI = [("conv-debug", None), ("ops-prof-conv-3x3-cudnn-boda", 37)]
 

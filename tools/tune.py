@@ -214,8 +214,8 @@ def main():
             cand = []
             if not (kind == 0 and s.flops() > args.max_flop_sgemm):
                 for ci, cn in enumerate(names[kind]):
-                    if args.cfg_re and not re.search(args.cfg_re, cn):
-                        continue
+                    if (args.cfg_re and not re.search(args.cfg_re, cn)) or cn == "ref64":
+                        continue  # (ref64: the double-accumulating known-good kernel, never routed)
                     nkt = -(-K // bk_of(cn))
                     if cn.startswith("dm"):  # multi-channel direct conv: S = grid mode as stream-K
                         if kind == 1 and cn.startswith("dm%d" % s.KY) and s.KX == s.KY and s.sy == s.sx == 1:
