@@ -325,6 +325,20 @@ def main():
                 roof["traffic_source"] = tj.get("source")
         except (OSError, ValueError):
             pass
+    # the same kernel's average launch duration from the committed rocprofv3 --kernel-trace --stats
+    # summary of the graph-replayed step (tools/rocprof_dominant.py): the profile-derived fraction
+    # beside the bench's amortized one
+    rp = os.path.join(ROOT, "profiles", "rocprof_dominant.json")
+    if os.path.exists(rp):
+        try:
+            rj = json.load(open(rp))
+            if rj.get("kernel") == dom and rj.get("avg_ns"):
+                a_rp = roof["avg_flops_per_launch"] / (rj["avg_ns"] * 1e-9)
+                roof["avg_launch_ms_rocprof"] = round(rj["avg_ns"] * 1e-6, 4)
+                roof["frac_rocprof"] = round(a_rp / runner.PEAK_FP32_FLOPS, 4)
+                roof["rocprof_source"] = rj.get("source")
+        except (OSError, ValueError, KeyError):
+            pass
 
     cpu = None
     if dd.rank == 0 and dd.world == 1 and not args.no_cpu_baseline:

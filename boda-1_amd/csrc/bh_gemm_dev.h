@@ -363,6 +363,7 @@ struct cfg_t {
   int gv_cx = 1;      // gv: interleaved column tiles (1x1, a lane's gv_cx pixels per load)
   int fcv = 0;        // gv: batch-streaming ipconv kernel (bh_gv.hip fcv_kernel), batch <= BN
   int ref64 = 0;      // double-accumulating known-good kernel (bh_ref64.hip), never tuned in
+  int k1n = 0;        // dc == 3: the pixels-on-N form (bh_k1s.hip k1n_kernel; gv_cx pixels per lane)
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and

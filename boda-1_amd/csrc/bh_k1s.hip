@@ -262,6 +262,271 @@ __global__ __launch_bounds__(NW * 64) void k1s_kernel(GemmArgs p) {
   KT(4);
 }
 
+// k1n: the same resident bank and register-streamed input with the MFMA's roles swapped (round 5).
+// PMC of k1s on 20x96x54^2 -> 96 (profiles/r04/pmc_k1s.json): 5.1 VALU + 4.0 SALU per MFMA, most of
+// it in the epilogue -- with pixels on the M side a lane's accumulators are 4 consecutive pixels of
+// one channel, which k1s transposes through LDS (ds writes / reads, a bias shuffle, per-element
+// fallbacks) to get 128-B store runs. Here the bank is the A operand (lane li: channel oc0 + 32 t +
+// li of bank row 2 s + kh, the same ds_read_b32 as k1s's B) and the input the B operand, so C is
+// [channel][pixel]: lane (li, kh) holds pixel column li of channels 32 t + 8 g + 4 kh + i, i.e. the
+// output rows are already in memory order:
+//  * a unit is 32 TN pixels; lane li owns TN adjacent pixels TN li .. + TN - 1 (column li of TN
+//    interleaved N tiles): one TN-wide load per k step feeds TM x TN MFMAs, and one TN-wide store
+//    per output row writes 32 x 4 TN contiguous bytes per half-wave (OH*OW % TN == 0, so a lane's
+//    pixels never straddle two images);
+//  * epilogue per tile and row: a bias (ds_read_b128 of 4 rows' biases), the add, the ReLU and one
+//    store at the lane's VGPR pixel offset + the row's scalar offset -- no transposes, no shuffles;
+//    rows past OC only in the last OC tile (a wave-uniform branch to the masked form).
+// S = 16 TM stores per unit (TN-wide), so (Q - 1) SC + 16 TM <= 63 bounds the configurations.
+template <int TN>
+__device__ __forceinline__ typename fvec<TN>::t ldv(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (TN == 1) return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  else if constexpr (TN == 2)
+    return __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  else return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+template <int TN, int AUX>
+__device__ __forceinline__ void stv(typename fvec<TN>::t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (TN == 1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, AUX);
+  else if constexpr (TN == 2)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) uint32_t, v), r, voff,
+                                          soff, AUX);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), r, voff,
+                                           soff, AUX);
+}
+
+// max(x, floor) as one v_max_f32 (fmaxf adds a canonicalizing v_max per operand in IEEE mode);
+// floor is 0 (ReLU) or -inf (none); the accumulators hold no NaN of interest to quiet
+__device__ __forceinline__ float relu_floor(float x, float floor) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(floor), "v"(x));
+  return r;
+}
+
+template <int TM, int TN, int KC, int Q, int NW>
+__global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
+  constexpr int OCT = 32 * TM;           // output channels of the block
+  constexpr int UPX = 32 * TN;           // pixels per unit
+  constexpr int SC = KC / 2;             // k steps (and input loads per lane) per chunk
+  constexpr int S = 16 * TM;             // TN-wide stores per lane per unit
+  constexpr int PF = 3;                  // LDS fragment prefetch (steps)
+  constexpr int WPC = KC * OCT / 4;      // 16-B bank pieces per chunk
+  constexpr int LWC = (WPC + NW * 64 - 1) / (NW * 64);
+  constexpr int BREG = ((OCT + 63) / 64) * 64;  // bias floats in LDS (whole 64-lane DMAs)
+  static_assert(TM >= 1 && TM <= 3 && KC % 2 == 0 && (TN == 1 || TN == 2 || TN == 4), "tile");
+  static_assert(Q >= 2 && (Q - 1) * SC + S <= 63, "vmcnt range");
+  static_assert(SC % (PF + 1) == 0, "fragment ring period divides a chunk");
+  static_assert(BREG <= NW * 64, "one bias DMA per wave at most");
+  typedef typename fvec<TN>::t xv;
+  // the bank slice [IC][OCT] (packed-bank rows, columns oc0 ..), then the tile's biases
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t l8 = blockIdx.x >> 3;
+  const uint32_t oct = l8 % p.tiles_m;
+  const uint32_t gi = (l8 / p.tiles_m) * 8 + (blockIdx.x & 7);
+  const uint32_t wg = (gridDim.x / p.tiles_m) * NW;  // waves per OC tile
+  const uint32_t oc0 = oct * OCT;
+  const uint32_t npu = (p.N + UPX - 1) / UPX, nch = p.K / KC;
+  const uint32_t lds_w = p.K * OCT;
+  const uint32_t hw4 = p.HW * 4u, ohw4 = p.OHW * 4u;
+  float *const bl = wl + lds_w;
+
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsx = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+
+  // biases of the tile (zeros past OC or without biases): older than every wait's count
+  if (64 * wave < BREG) {
+    const uint32_t oc = oc0 + 64 * wave + lane;
+    dma4(rsbias, bl + 64 * wave, oob_unless(oc < p.M, oc * 4u));
+  }
+  uint32_t wsrc[LWC];
+#pragma unroll
+  for (int j = 0; j < LWC; ++j) {
+    const uint32_t e = (uint32_t)((j * NW + wave) * 64 + lane), r = e / (OCT / 4), q = e % (OCT / 4);
+    wsrc[j] = e < (uint32_t)WPC ? oob_unless(oc0 + 4 * q < p.lda, (r * p.lda + oc0 + 4 * q) * 4u) : 0xffffffffu;
+  }
+  auto issue_w = [&](uint32_t c) {
+#pragma unroll
+    for (int j = 0; j < LWC; ++j)
+      if (wsrc[j] != 0xffffffffu)
+        dma16s(rsw, wl + (size_t)c * KC * OCT + (j * NW + wave) * 256, wsrc[j], c * KC * p.lda * 4u);
+  };
+  // lane li's first pixel of unit pu and its input offset (channel kh); past the op: misses
+  auto ubase = [&](uint32_t pu) -> uint32_t {
+    const uint32_t n = pu * UPX + TN * li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    return oob_unless((pu < npu) & (n < p.N), (img * p.ICHW + pix + kh * p.HW) * 4u);
+  };
+  xv xr[Q][SC];
+  auto issue = [&](int q, uint32_t base, uint32_t c) {
+    const uint32_t vb = base + c * KC * hw4;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) xr[q][s] = ldv<TN>(rsx, vb, 2 * s * hw4);
+  };
+  uint32_t pu = gi * NW + wave;
+  uint32_t bcur = ubase(pu), bnext = ubase(pu + wg);
+#pragma unroll
+  for (int q = 0; q < Q - 1; ++q) {
+    issue_w(q);
+    issue(q, bcur, q);
+  }
+  // S dropped stores: the first unit has the VMEM sequence of every later one
+#pragma unroll
+  for (int s = 0; s < S; ++s) __builtin_amdgcn_raw_buffer_store_b32(0u, rso, OOB, 0, 0);
+
+  f32x16 acc[TM][TN];
+  float wf[PF + 1][TM];
+  const float *const wb = wl + kh * OCT + li;
+  auto frag = [&](float (&w)[TM], uint32_t c, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) w[t] = wb[(c * KC + 2 * s) * OCT + 32 * t];
+  };
+  // the tile's biases as MFMA C operands: the first step of every unit accumulates onto them
+  // (no zeroing, no bias add in the epilogue); row 8 (e / 4) + 4 kh + e % 4 of tile t
+  f32x16 biasv[TM];
+  auto chunk = [&](int r, uint32_t cq, bool first, bool u0) {
+    if (first && r < Q - 1) vm_wait<(Q - 2) * SC + S>();
+    else vm_wait<(Q - 2) * SC>();
+    if (u0) {
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < PF; ++s) frag(wf[s], cq + r, s);
+      if (first && r == 0) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4v b4 = *(const f32x4v *)(bl + 32 * t + 8 * g + 4 * kh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) biasv[t][4 * g + e] = b4[e];
+          }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const uint32_t c2 = cq + (uint32_t)(r + Q - 1);
+      const bool nx = c2 >= nch;
+      if (u0 && !nx) issue_w(c2);
+      issue((r + Q - 1) % Q, nx ? bnext : bcur, nx ? c2 - nch : c2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t c = cq + (uint32_t)r, cn = c + 1 == nch ? 0u : c + 1;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {
+      if (s + PF < SC) frag(wf[(s + PF) % (PF + 1)], c, s + PF);
+      else if (!u0) frag(wf[(s + PF) % (PF + 1)], cn, s + PF - SC);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s % (PF + 1)][t], vget<TN>(xr[r % Q][s], j),
+                                                           first && r == 0 && s == 0 ? biasv[t] : acc[t][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const bool full_m = oc0 + OCT <= p.M;
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  // epilogue: row 8 g + 4 kh + i of tile t is channel oc0 + 32 t + 8 g + 4 kh + i; the lane's half
+  // (4 kh rows) goes into its VGPR offset, the rest of the row into the scalar soffset
+  // the epilogue's wave-uniform choices (mask, residual, store policy) are taken once per unit:
+  // branches per row cost a basic block per store
+  const float floor0 = p.relu ? 0.0f : -__builtin_inff();
+  auto epilogue = [&](auto masked, auto res, auto wt) {
+    // the rows' scalar offsets are made here, per unit (laundered stride: hoisted out of the unit
+    // loop, 16 TM of them spilled SGPRs into VGPR lanes)
+    uint32_t h4 = ohw4;
+    asm volatile("" : "+s"(h4));
+    const uint32_t so0 = oc0 * h4;
+    const uint32_t n = pu * UPX + TN * li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    const uint32_t ob = oob_unless((pu < npu) & (n < p.N), (img * p.OCOHW + pix) * 4u + (uint32_t)(4 * kh) * h4);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t so = so0 + (uint32_t)(32 * t + 8 * g + i) * h4;
+          uint32_t o = ob;
+          if constexpr (decltype(masked)::value)
+            o = oob_unless(oc0 + (uint32_t)(32 * t + 8 * g + 4 * kh + i) < p.M, ob);
+          xv v;
+          if constexpr (TN == 1) v = acc[t][0][4 * g + i];
+          else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) v[j] = acc[t][j][4 * g + i];
+          }
+          if constexpr (decltype(res)::value) v += ldv<TN>(rsr, o, so);
+          if constexpr (TN == 1) v = relu_floor(v, floor0);
+          else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) v[j] = relu_floor(v[j], floor0);
+          }
+          if constexpr (decltype(wt)::value) stv<TN, AUX_SC1>(v, rso, o, so);
+          else stv<TN, AUX_OUT>(v, rso, o, so);
+        }
+      }
+  };
+  auto epilogue_m = [&](auto masked) {
+    if (p.res) {
+      if (p.wt) epilogue(masked, std::true_type{}, std::true_type{});
+      else epilogue(masked, std::true_type{}, std::false_type{});
+    } else {
+      if (p.wt) epilogue(masked, std::false_type{}, std::true_type{});
+      else epilogue(masked, std::false_type{}, std::false_type{});
+    }
+  };
+
+  for (bool u0 = true;; u0 = false) {
+    if (u0) {
+#pragma unroll
+      for (int r = 0; r < Q; ++r) chunk(r, 0, true, true);
+      for (uint32_t cq = Q; cq < nch; cq += Q) {
+#pragma unroll
+        for (int r = 0; r < Q; ++r) chunk(r, cq, false, true);
+      }
+#pragma unroll
+      for (int s = 0; s < PF; ++s) frag(wf[s], 0, s);
+    } else {
+#pragma unroll
+      for (int r = 0; r < Q; ++r) chunk(r, 0, true, false);
+      for (uint32_t cq = Q; cq < nch; cq += Q) {
+#pragma unroll
+        for (int r = 0; r < Q; ++r) chunk(r, cq, false, false);
+      }
+    }
+    // every unit issues exactly S stores (dropped where masked or past the op): the waits count them
+    if (full_m) epilogue_m(std::false_type{});
+    else epilogue_m(std::true_type{});
+    pu += wg;
+    if (pu >= npu) break;
+    bcur = bnext;
+    bnext = ubase(pu + wg);
+  }
+  vm_wait<0>();
+}
+
+template <int TM, int TN, int KC, int Q, int NW>
+cfg_t k1n_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * TN * NW, KC, 64 * NW, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = k1n_kernel<TM, TN, KC, Q, NW>;
+  c.dc = 3;
+  c.dc_ky = 1;
+  c.dc_kx = 1;
+  c.dc_ci = KC;
+  c.dc_rin = Q;
+  c.gv_cx = TN;
+  c.k1n = 1;
+  return c;
+}
+
 template <int TM, int KC, int Q, int NW, int DBG = 0>
 cfg_t k1s_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * NW, KC, 64 * NW, {}, 1};
@@ -287,6 +552,15 @@ std::vector<cfg_t> k1s_cfgs() {
       k1s_cfg<4, 16, 4, 4>("ks128c16q4"),   k1s_cfg<1, 16, 4, 4>("ks32c16q4"),
       k1s_cfg<2, 32, 3, 8>("ks64c32q3w8"),  k1s_cfg<3, 32, 3, 8>("ks96c32q3w8"),
       k1s_cfg<1, 32, 3, 8>("ks32c32q3w8"),  k1s_cfg<1, 16, 4, 8>("ks32c16q4w8"),
+      // k1n <TM, TN, KC, Q, NW>: kn<OC tile>p<pixels per unit>c<KC>q<Q>w<NW>
+      k1n_cfg<1, 1, 16, 4, 8>("kn32p32c16q4w8"),   k1n_cfg<1, 2, 16, 4, 8>("kn32p64c16q4w8"),
+      k1n_cfg<1, 4, 16, 4, 4>("kn32p128c16q4w4"),  k1n_cfg<1, 2, 32, 3, 8>("kn32p64c32q3w8"),
+      k1n_cfg<1, 1, 32, 3, 8>("kn32p32c32q3w8"),   k1n_cfg<2, 1, 16, 3, 8>("kn64p32c16q3w8"),
+      k1n_cfg<2, 2, 16, 3, 8>("kn64p64c16q3w8"),   k1n_cfg<2, 2, 16, 4, 8>("kn64p64c16q4w8"),
+      k1n_cfg<2, 2, 32, 2, 8>("kn64p64c32q2w8"),   k1n_cfg<2, 4, 16, 3, 4>("kn64p128c16q3w4"),
+      k1n_cfg<2, 2, 16, 4, 4>("kn64p64c16q4w4"),   k1n_cfg<3, 1, 8, 4, 8>("kn96p32c8q4w8"),
+      k1n_cfg<3, 2, 8, 4, 8>("kn96p64c8q4w8"),     k1n_cfg<3, 2, 16, 2, 8>("kn96p64c16q2w8"),
+      k1n_cfg<3, 2, 8, 4, 4>("kn96p64c8q4w4"),
 #ifdef BH_KTRACE
       k1s_cfg<3, 32, 3, 4, 1>("xks96c32q3_noload"), k1s_cfg<3, 32, 3, 4, 2>("xks96c32q3_nomfma"),
       k1s_cfg<3, 32, 3, 4, 4>("xks96c32q3_nostore"), k1s_cfg<3, 32, 3, 4, 7>("xks96c32q3_none"),
@@ -297,7 +571,8 @@ std::vector<cfg_t> k1s_cfgs() {
 // Launch a resident-bank 1x1 configuration (p filled by launch_conv with a = packed bank): UNSUP
 // unless the shape is a stride-1 unpadded 1x1 conv whose K is a whole number of trips (Q chunks
 // of KC channels) and whose bank slice fits the LDS. splits: 0 = two blocks per CU where they
-// fit, 1..4 = blocks per CU.
+// fit, 1..4 = blocks per CU (a persistent grid: a wave takes every wg-th unit), 8 = one unit per
+// wave (the whole grid queued: no wave runs two units while another SIMD idles in the tail).
 int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY, uint32_t KX, uint32_t sy,
                uint32_t sx, uint32_t splits, bool first) {
   (void)B;
@@ -306,8 +581,17 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   const uint32_t KC = (uint32_t)c.dc_ci, Q = (uint32_t)c.dc_rin, NT = (uint32_t)c.NT;
   if (p.K % KC || (p.K / KC) % Q)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a whole number of ") + c.name + " trips");
-  // the bank slice [IC][OCT] and one [32][36] epilogue staging tile per wave
-  const uint64_t lds = ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;
+  // k1n: a lane's gv_cx pixels lie in one image (OH*OW % gv_cx == 0) and its vector loads / stores
+  // are aligned
+  const uint32_t tn = (uint32_t)c.gv_cx;
+  if (c.k1n && tn > 1 &&
+      (p.OHW % tn || (uintptr_t)p.b % (4u * tn) || (uintptr_t)p.c % (4u * tn) || (uintptr_t)p.res % (4u * tn)))
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs OH*OW % " + std::to_string(tn) +
+                                  " == 0 and aligned input / output rows");
+  // k1s: the bank slice [IC][OCT] and one [32][36] epilogue staging tile per wave; k1n: the bank
+  // slice and the tile's biases (whole 64-float DMAs)
+  const uint64_t lds = c.k1n ? ((uint64_t)p.K * c.BM + (uint64_t)((c.BM + 63) / 64) * 64) * 4
+                             : ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;
   if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: bank slice too large for ") + c.name);
   const uint64_t out_bytes = (uint64_t)p.OCOHW * (p.N / p.OHW) * 4;
   if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the k1s kernel");
@@ -318,8 +602,9 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, c.NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
   const uint32_t oct = (p.M + c.BM - 1) / c.BM;
-  const uint32_t npu = (p.N + 31) / 32, nw = NT / 64;
-  uint32_t bpc = splits ? splits : 2;
+  const uint32_t npu = (p.N + 32 * (c.k1n ? tn : 1u) - 1) / (32 * (c.k1n ? tn : 1u)), nw = NT / 64;
+  const bool full = splits >= 8;
+  uint32_t bpc = splits && !full ? splits : 2;
   bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));
   const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
   // blocks per OC tile: enough waves for every pixel unit, at most the CUs' share; a multiple of 8
@@ -328,6 +613,7 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   uint64_t per = std::max<uint64_t>(1, ((uint64_t)ncu * bpc) / oct);
   per = std::min<uint64_t>(per, (npu + nw - 1) / nw);
   per = per >= 8 ? per / 8 * 8 : 8;
+  if (full) per = ((npu + nw - 1) / nw + 7) / 8 * 8;
   const uint64_t G = per * oct;
   if (G >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: k1s grid too large");
   p.tiles_m = oct;

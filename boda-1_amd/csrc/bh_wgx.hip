@@ -838,7 +838,7 @@ int launch_wx_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uint3
 }
 
 // Launch a position-split Winograd configuration: UNSUP unless a stride-1 R x R conv (R = the
-// configuration's) with pad <= R / 2, IC % 4 == 0, IC <= 128 for F(4x4,3x3) and <= 96 for F(2x2,5x5)
+// configuration's) with pad <= R / 2, IC % 4 == 0, IC <= 64 for F(4x4,3x3) and <= 96 for F(2x2,5x5)
 // (their fp32 element error), whose strips fit the configuration's slot. u: the bank of the configuration's
 // form (6x6: wx_pack; 4x4: bh_wino.hip's). One block per unit (whole units), or (dc_wpm) a resident
 // stream-K grid over the (unit, stage) iterations.
@@ -853,10 +853,11 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   if (IC % XC) return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs IC % 4 == 0");
   // the 6x6 forms' element error grows as sqrt(IC) (the transformed-domain sum dominates it): measured
   // against float64 with Boda's element metric, F(4x4,3x3) reaches 1.1e-3 at IC 64 and 2.2e-3 at
-  // IC 256, F(2x2,5x5) 0.8e-3 at IC 32 and 1.1-2.1e-3 at IC 96; the caps keep a forced
+  // IC 256 (2.15e-3 already at IC 128 on 20 x 128 x 28^2 -> 192, round 5's ops-prof sweep),
+  // F(2x2,5x5) 0.8e-3 at IC 32 and 1.1-2.1e-3 at IC 96; the caps keep a forced
   // configuration near Boda's Winograd tolerance (2e-3, src/rtc_prof.cc:314-319), the tuner routes
   // only ops measured inside it
-  const uint32_t ic_cap = N == 4 ? 0u : (MO == 4 ? 128u : 96u);
+  const uint32_t ic_cap = N == 4 ? 0u : (MO == 4 ? 64u : 96u);
   if (ic_cap && IC > ic_cap)
     return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " keeps IC <= " + std::to_string(ic_cap) +
                                   " (fp32 element error of the 6x6 transforms)");

@@ -31,7 +31,8 @@ SHAPES = {
              ops.ConvShape(2, 1, 60, 41, 70, 7, 7, 2, 2, 1, 3),
              ops.ConvShape(1, 4, 97, 100, 33, 7, 7, 2, 2, 2, 0),
              ops.ConvShape(2, 2, 40, 44, 20, 7, 7, 2, 2, 1, 1),    # W % 4 == 0, pad 1 (16-B strip)
-             ops.ConvShape(2, 3, 128, 128, 40, 7, 7, 2, 2, 3, 3)],  # W % 4 == 0, 2-row pixel tiles
+             ops.ConvShape(2, 3, 128, 128, 40, 7, 7, 2, 2, 3, 3),   # W % 4 == 0, 2-row pixel tiles
+             ops.ConvShape(2, 2, 90, 200, 40, 7, 7, 2, 2, 3, 3)],   # W % 4 == 0, IC <= 3: resident-weight 16-B strips
     (11, 4): [ops.ConvShape(2, 3, 227, 227, 96, 11, 11, 4, 4, 0, 0),
               ops.ConvShape(1, 3, 224, 224, 96, 11, 11, 4, 4, 0, 0),
               ops.ConvShape(2, 2, 60, 71, 40, 11, 11, 4, 4, 2, 1),
@@ -39,7 +40,7 @@ SHAPES = {
               ops.ConvShape(1, 4, 100, 224, 40, 11, 11, 4, 4, 1, 1),  # W % 4 == 0, pad 1 (16-B strip)
               ops.ConvShape(1, 3, 100, 516, 96, 11, 11, 4, 4, 0, 0),  # op_sigs' 516-wide stem rows
               ops.ConvShape(2, 2, 60, 300, 20, 11, 11, 4, 4, 2, 2),
-              ops.ConvShape(2, 3, 64, 128, 40, 11, 11, 4, 4, 2, 2)],  # W % 4 == 0, IC 3: resident-weight 16-B strips
+              ops.ConvShape(2, 3, 60, 220, 40, 11, 11, 4, 4, 2, 2)],  # W % 4 == 0, IC 3: resident-weight 16-B strips
     (6, 2): [ops.ConvShape(1, 3, 100, 516, 40, 6, 6, 2, 2, 0, 0),    # op_sigs' 516-wide 6x6 s2 stem rows
              ops.ConvShape(2, 2, 64, 132, 20, 6, 6, 2, 2, 1, 1),     # 3-row pixel tiles, pad 1
              ops.ConvShape(1, 4, 40, 60, 33, 6, 6, 2, 2, 0, 2),

@@ -1,7 +1,8 @@
-"""Resident-bank 1x1 kernels (bh_k1s.hip, configs ks*) against the oracle.
+"""Resident-bank 1x1 kernels (bh_k1s.hip, configs ks* and their pixels-on-N form kn*) against the oracle.
 
-Each ks configuration serves unpadded stride-1 1x1 convs whose input channels are a whole
-number of its trips (Q chunks of KC channels: ks<OCT>c<KC>q<Q>). It is forced with bh_tune_set
+Each ks / kn configuration serves unpadded stride-1 1x1 convs whose input channels are a whole
+number of its trips (Q chunks of KC channels: ks<OCT>c<KC>q<Q>, kn<OCT>p<pixels per unit>c<KC>q<Q>;
+a kn unit of 32 TN pixels needs OH*OW % TN == 0, TN = pixels / 32). It is forced with bh_tune_set
 on such shapes: pixel units that run across image boundaries (13x13, 7x9, 6x6 images), quads
 that straddle an image (OH*OW % 4 != 0: element stores), ragged output channels and several OC
 tiles, fewer pixels than one unit, and every blocks-per-CU setting the tuner may pick -- checked
@@ -21,18 +22,28 @@ from test_gpu_conv import run_conv
 
 pytestmark = pytest.mark.gpu
 
-KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith("ks")]
+KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("ks", "kn"))]
 
 
 def trip_of(name):
-    kc, q = map(int, re.match(r"ks\d+c(\d+)q(\d+)", name).groups())
+    kc, q = map(int, re.match(r"k[sn]\d+(?:p\d+)?c(\d+)q(\d+)", name).groups())
     return kc * q
 
 
+def tn_of(name):
+    """Pixels per lane of a kn configuration (1 for ks)."""
+    m = re.match(r"kn\d+p(\d+)", name)
+    return int(m.group(1)) // 32 if m else 1
+
+
 def fits(name, ic):
-    """The bank slice [IC][OCT] and the waves' [32][36] epilogue tiles fit the LDS."""
+    """ks: the bank slice [IC][OCT] and the waves' [32][36] epilogue tiles fit the LDS; kn: the
+    bank slice and the tile's biases (whole 64-float DMAs)."""
+    oct_ = int(re.match(r"k[sn](\d+)", name).group(1))
+    if name.startswith("kn"):
+        return (ic * oct_ + -(-oct_ // 64) * 64) * 4 <= 160 * 1024
     nw = 8 if name.endswith("w8") else 4
-    return (ic * int(re.match(r"ks(\d+)", name).group(1)) + nw * 32 * 36) * 4 <= 160 * 1024
+    return (ic * oct_ + nw * 32 * 36) * 4 <= 160 * 1024
 
 
 def k1(b, ic, h, w, oc):
@@ -41,7 +52,8 @@ def k1(b, ic, h, w, oc):
 
 SHAPES = [k1(2, 96, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(1, 96, 28, 28, 130), k1(5, 192, 6, 6, 64),
           k1(2, 96, 7, 9, 40), k1(2, 64, 14, 14, 64), k1(1, 128, 27, 27, 256), k1(3, 256, 7, 7, 48),
-          k1(1, 288, 5, 5, 33), k1(1, 64, 1, 1, 20), k1(4, 384, 13, 13, 100)]
+          k1(1, 288, 5, 5, 33), k1(1, 64, 1, 1, 20), k1(4, 384, 13, 13, 100),
+          k1(2, 192, 12, 12, 72), k1(3, 128, 10, 10, 100)]  # OH*OW % 4 == 0, ragged OC: kn's masked rows
 
 
 def check(out, s):
@@ -59,7 +71,7 @@ def test_ks_config(dev, cn):
         for s in SHAPES:
             if s.IC % trip_of(cn):
                 continue
-            if not fits(cn, s.IC):
+            if not fits(cn, s.IC) or (s.OH * s.OW) % tn_of(cn):
                 dev.tune_set(1, ci, 0)
                 with pytest.raises(boda_hip.UnsupportedError):
                     run_conv(dev, s)
@@ -88,12 +100,17 @@ def test_ks_rejects(dev, cn):
                   k1(1, t + 16, 13, 13, 16)):                          # K not a whole number of trips
             with pytest.raises(boda_hip.UnsupportedError):
                 run_conv(dev, s)
+        if tn_of(cn) > 1:  # a lane's pixels would straddle two images
+            with pytest.raises(boda_hip.UnsupportedError):
+                run_conv(dev, k1(2, t, 7, 7, 16))
     finally:
         dev.tune_set(1, -1, 0)
 
 
-@pytest.mark.parametrize("cn", [n for n in KS if n in ("ks96c32q3", "ks64c16q4")])
-@pytest.mark.parametrize("s", [k1(2, 192, 14, 14, 96), k1(3, 192, 13, 13, 70)])
+@pytest.mark.parametrize("cn,s", [(cn, s) for cn in ("ks96c32q3", "ks64c16q4", "kn96p32c8q4w8", "kn64p64c16q3w8",
+                                                    "kn32p128c16q4w4")
+                                  for s in (k1(2, 192, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(2, 192, 12, 12, 72))
+                                  if (s.OH * s.OW) % tn_of(cn) == 0])
 def test_ks_residual_and_slab(dev, cn, s):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)
     try:

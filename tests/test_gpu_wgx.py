@@ -1,7 +1,7 @@
 """Position-split Winograd kernels (bh_wgx.hip, configs wx*) against the oracle.
 
 wx43* is F(4x4, 3x3) and wx23* F(2x2, 3x3) for stride-1 3x3 convs, wx25* F(2x2, 5x5) for stride-1
-5x5 convs (square padding <= R / 2, IC % 4 == 0; the 6x6 forms also IC <= 128 / 96). They are forced with
+5x5 convs (square padding <= R / 2, IC % 4 == 0; the 6x6 forms also IC <= 64 / 96). They are forced with
 bh_tune_set on shapes whose 32-tile units run across tile rows and images (outputs that are not a
 multiple of the 4- / 2-wide tile, a last unit only partly filled), ragged output channels (not a
 multiple of the 64- / 128-channel tile, nor of 32), unpadded and non-square inputs. The result is
@@ -40,7 +40,8 @@ SHAPES3 = [
     C(1, 24, 40, 62, 50, 3, 3, 1, 1, 1, 1),
     C(2, 256, 13, 13, 384, 3, 3, 1, 1, 1, 1),  # a conv-set layer (many stages)
     C(1, 512, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # long K (wx23; over the 6x6 forms' cap)
-    C(1, 128, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # IC at F(4x4,3x3)'s cap
+    C(1, 128, 14, 14, 64, 3, 3, 1, 1, 1, 1),   # IC over F(4x4,3x3)'s cap (wx23 only)
+    C(2, 64, 14, 14, 64, 3, 3, 1, 1, 1, 1),    # IC at F(4x4,3x3)'s cap
 ]
 SHAPES5 = [
     C(2, 16, 27, 27, 96, 5, 5, 1, 1, 2, 2),    # the AlexNet conv2 geometry, odd output

@@ -12,3 +12,6 @@ tools/gpu_job.sh \
   traffic 600 tools/traffic.sh gpurun_out/traffic gpurun_out/traffic.json :: \
   profgraph 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_graph -o bench -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --vendor off --op-timing events
+# then, here: the dominant kernel's rocprof average for bench.py's roofline.frac_rocprof
+#   python tools/rocprof_dominant.py <the profgraph stats csv> <roofline.kernel> "<its template instance>" \
+#     > profiles/rocprof_dominant.json
