@@ -83,7 +83,9 @@ __device__ __forceinline__ void dc_static_for(F &&f) {
 // instructions: the strip's dword DMAs were 0.34 issues per MFMA at 11x11 s4); column c of the
 // strip then holds input x = c - PXA with PXA = 4 (0 without horizontal padding), so pieces start
 // on 16-B input boundaries
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0>
+// PFO > 0: the LDS fragment prefetch distance (steps) instead of the default for the tile (round 5: the
+// stage loop waits on its fragment reads, one s_waitcnt per MFMA)
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0, int PFO = 0>
 __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int NW = 4;
   constexpr int NPX = NW * 32 * TN, OCT = 32 * TM;
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
   constexpr int LW = LWA + LWB + 1;
   static_assert(D >= 2 && (D - 2) * LW <= 63, "vmcnt range");
   static_assert(OCT % 4 == 0 && OCT <= BREG, "16-B weight pieces, biases of one tile");
-  constexpr int PF = TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3);  // LDS fragment prefetch distance (steps)
+  constexpr int PF = PFO > 0 ? PFO : (TM * TN >= 4 ? 1 : (TM * TN >= 2 ? 2 : 3));  // LDS fragment prefetch distance (steps)
   constexpr int IS = (KK2 + 1) / 2 > 1 ? (KK2 + 1) / 2 : 1;     // steps the next stage's DMAs are spread over
   // epilogue: a lane's accumulators hold 4 consecutive pixels of one output channel per
   // register quad (the MFMA's rows are pixels), stored as NST float4 pieces per lane, deferred
@@ -448,7 +450,10 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 //  * a step is as in dc_kernel: A = resident weights (one ds_read_b32 per tile), B = the strip at a
 //    compile-time tap offset from one of three per-lane bases; the next stage's strip DMAs spread
 //    over the first IS steps, the previous tile's output stores deferred into the first steps.
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX>
+// DBG (diagnostic builds in the instrumented library only; wrong results by design): bit 0 = no strip DMA
+// after the prologue, 1 = no MFMA, 2 = no output stores, 3 = no stage barrier, 4 = no B (strip) fragment
+// reads, 5 = no A (weight) fragment reads
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0>
 __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   constexpr int NT = NW * 64, NPX = NW * 32, OCT = 32 * TM;
   constexpr int KK = KY * KX, KK2 = (KK + 1) / 2;
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   constexpr int SREG = LWB * NT * PW;                       // floats per strip slot
   static_assert(D >= 2 && (D - 2) * LWB <= 63, "vmcnt range");
   static_assert(OCT % 4 == 0 && BREG <= NT, "16-B weight pieces, one bias DMA per wave at most");
-  constexpr int PF = TM >= 2 ? 2 : 3;                       // LDS fragment prefetch distance (steps)
+  constexpr int PF = PFO > 0 ? PFO : (TM >= 2 ? 2 : 3);    // LDS fragment prefetch distance (steps)
   constexpr int IS = (KK2 + 1) / 2 > 1 ? (KK2 + 1) / 2 : 1;   // steps the next stage's DMAs are spread over
   constexpr int NST = TM * 4;                               // deferred float4 stores per lane and tile
   constexpr int ISS = KK2 > 2 * NST ? 2 * NST : KK2;
@@ -541,7 +546,7 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   auto store_one = [&](int q) {  // deferred float4 piece q = (t, gq) of the previous tile
     const int t = q / 4, gq = q % 4;
     const uint32_t px = dpx + (uint32_t)(8 * gq);
-    const uint32_t off = dbase[t] + (uint32_t)(8 * gq) * 4u;
+    const uint32_t off = (DBG & 4) ? OOB : dbase[t] + (uint32_t)(8 * gq) * 4u;
     if (px + 4 <= dhw) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dval[q]),
                                              rso, off, 0, AUX_OUT);
@@ -571,10 +576,10 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
                          Sb + poff + (int)(hsel & (uint32_t)(DPAD * 4))};
     auto frag = [&](int s, float (&a)[TM], float &b) {
 #pragma unroll
-      for (int t = 0; t < TM; ++t) a[t] = Ab[s * OCT + 32 * t];
+      for (int t = 0; t < TM; ++t) a[t] = (DBG & 32) ? (float)(s + t) : Ab[s * OCT + 32 * t];
       const int k0 = dc_koff<KX, WPM>(s, KK) * 4;
       const int kind = KK2 + s >= KK ? 2 : (s % KX < KX - CSH ? 0 : 1);
-      b = *(const float *)(bs[kind] + k0);
+      b = (DBG & 16) ? (float)s : *(const float *)(bs[kind] + k0);
     };
     float a[PF + 1][TM], b[PF + 1];
 #pragma unroll
@@ -584,10 +589,14 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
       if (s + PF < KK2) frag(s + PF, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < TM; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)], a[s % (PF + 1)][t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TM; ++t) {
+        if constexpr ((DBG & 2) != 0) acc[t][s % 16] += b[s % (PF + 1)] * a[s % (PF + 1)][t];
+        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)], a[s % (PF + 1)][t], acc[t], 0, 0, 0);
+      }
+      if constexpr ((DBG & 1) == 0) {
 #pragma unroll
-      for (int q = (s * LWB + IS - 1) / IS; q < ((s + 1) * LWB + IS - 1) / IS && q < LWB; ++q) issue_one(q, islot, ic_issue);
+        for (int q = (s * LWB + IS - 1) / IS; q < ((s + 1) * LWB + IS - 1) / IS && q < LWB; ++q) issue_one(q, islot, ic_issue);
+      }
       if (dstores) {
 #pragma unroll
         for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
@@ -607,6 +616,15 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   }
   const bool vec = !p.res;
   const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  // the tile's biases start every tile's accumulators (no bias add in the epilogue); the ReLU is one
+  // v_max against a wave-uniform floor (0, or -inf without ReLU). Once per kernel: every DMA so far
+  // (weights, biases, the prologue's strips) landed, every wave's
+  vm_wait<0>();
+  __syncthreads();
+  float biasr[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) biasr[t] = bres[32 * t + li];
+  const float floor0 = p.relu ? 0.0f : -__builtin_inff();
   bool pending = false;
   int slot = 0;
   uint32_t g = 0;
@@ -622,11 +640,12 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+      for (int r = 0; r < 16; ++r) acc[t][r] = biasr[t];
     for (uint32_t ic = 0; ic < p.IC; ++ic, ++g) {
       vm_wait<(D - 2) * LWB>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // stage g (and, the first time, the weights) landed; all done with g-1
+      if (!(DBG & 8) || (i == 0 && ic == 0))
+        __builtin_amdgcn_s_barrier();  // stage g (and, the first time, the weights) landed; all done with g-1
       asm volatile("" ::: "memory");
       if (i == 0 && ic == 0) KT(1);
       compute(slot, slot == 0 ? D - 1 : slot - 1, ic, g + D - 1, pending);
@@ -644,16 +663,12 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
         const uint32_t m = oc0 + 32 * t + li;
-        const float bb = bres[32 * t + li];
         dbase[t] = oob_unless(m < p.M, (obase + m * p.OHW + dpx) * 4u);
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           f32x4v v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x = acc[t][4 * gq + e] + bb;
-            v[e] = (p.relu && x < 0.0f) ? 0.0f : x;
-          }
+          for (int e = 0; e < 4; ++e) v[e] = relu_floor(acc[t][4 * gq + e], floor0);
           dval[t * 4 + gq] = v;
         }
       }
@@ -667,14 +682,13 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
         const uint32_t m = oc0 + 32 * t + li;
-        const float bb = bres[32 * t + li];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const uint32_t px = p0 + (uint32_t)(wave * 32 + 8 * (r >> 2) + 4 * kh + (r & 3));
           const uint32_t o = oob_unless((m < p.M) & (px < p.OHW), (obase + m * p.OHW + px) * 4u);
-          float x = acc[t][r] + bb;
+          float x = acc[t][r];
           if (p.res) x += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, o, 0, 0));
-          x = (p.relu && x < 0.0f) ? 0.0f : x;
+          x = relu_floor(x, floor0);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), rso, o, 0, AUX_OUT);
         }
       }
@@ -687,10 +701,10 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #endif
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0>
 cfg_t dcr_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * NW, 2 * ((KY * KX + 1) / 2), 64 * NW, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dcr_kernel<KY, KX, S, WPM, RIN, TM, NW, D, V4, ICMAX>;
+  c.k[A_KVEC][B_DIRECT][0] = dcr_kernel<KY, KX, S, WPM, RIN, TM, NW, D, V4, ICMAX, DBG, PFO>;
   c.dc_ci = V4;
   c.dc = 1;
   c.dc_ky = KY;
@@ -702,10 +716,10 @@ cfg_t dcr_cfg(const char *name) {
   return c;
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int TN, int D, int V4 = 0, int PSL = 0, int PFO = 0>
 cfg_t dc_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 128 * TN, 2 * ((KY * KX + 1) / 2), 256, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D, V4, PSL>;
+  c.k[A_KVEC][B_DIRECT][0] = dc_kernel<KY, KX, S, WPM, RIN, TM, TN, D, V4, PSL, PFO>;
   c.dc_ci = V4;  // dc == 1: 16-B strip pieces (input rows of W % 4 == 0)
   c.dc = 1;
   c.dc_ky = KY;
@@ -734,6 +748,9 @@ std::vector<cfg_t> dc_cfgs() {
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2>("dc11s4x32d2"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3>("dc11s4x32d3"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 1>("dc11s4x32d2v"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 0, 0, 6>("dc11s4x32d2f6"), dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 1, 0, 6>("dc11s4x32d2vf6"),
+      dc_cfg<11, 11, 4, 228, 23, 1, 1, 2, 0, 0, 8>("dc11s4x32d2f8"),
+      dc_cfg<7, 7, 2, 236, 11, 2, 1, 2, 1, 0, 4>("dc7s2x64n128d2vf4"),
       dc_cfg<11, 11, 4, 228, 23, 1, 1, 3, 1>("dc11s4x32d3v"),
       dc_cfg<11, 11, 4, 228, 23, 3, 1, 2, 1>("dc11s4x96d2v"),
       // phase-split strips (conflict-free fragment reads; dword strip DMA)
@@ -759,6 +776,21 @@ std::vector<cfg_t> dc_cfgs() {
       dcr_cfg<7, 7, 2, 236, 13, 2, 8, 2, 1, 3>("dc7s2r64d2v"),
       dcr_cfg<7, 7, 2, 236, 13, 2, 8, 3, 1, 3>("dc7s2r64d3v"),
       dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3>("dc7s2r32d3v"),
+      // deeper fragment prefetch (f<PF>): the stage loops wait on their LDS reads
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 0, 6>("dc7s2r32d3vf6"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 0, 8>("dc7s2r32d3vf8"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 0, 6>("dc11s4r32d2f6"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 1, 3, 0, 6>("dc11s4r32d2vf6"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 0, 8>("dc11s4r32d2f8"),
+#ifdef BH_KTRACE
+      // diagnostic forms of dc7s2r32d3v / dc11s4r32d2 (wrong results by design; tools/job_dcrdiag.sh)
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 1>("xdc7r_nodma"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 2>("xdc7r_nomfma"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 4>("xdc7r_nostore"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 8>("xdc7r_nobar"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 16>("xdc7r_nob"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 32>("xdc7r_noa"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 48>("xdc7r_nolds"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 61>("xdc7r_onlymfma"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 63>("xdc7r_none"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 1>("xdc11r_nodma"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 2>("xdc11r_nomfma"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 8>("xdc11r_nobar"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 16>("xdc11r_nob"),
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 48>("xdc11r_nolds"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 61>("xdc11r_onlymfma"),
+#endif
       // VGG conv1_1 (3 x 224^2 -> 64, 3x3 s1 p1)
       dc_cfg<3, 3, 1, 228, 5, 2, 2, 3>("dc3s1x64d3"),
       dc_cfg<3, 3, 1, 228, 5, 1, 2, 3>("dc3s1x32d3"),

@@ -327,6 +327,14 @@ __device__ __forceinline__ void staged_epilogue(float *lds, f32x16 (&acc)[TM][TN
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// max(x, floor) as one v_max_f32 (fmaxf adds a canonicalizing v_max per operand in IEEE mode);
+// floor is 0 (ReLU) or -inf (none), wave-uniform; the accumulators hold no NaN of interest to quiet
+__device__ __forceinline__ float relu_floor(float x, float floor) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(floor), "v"(x));
+  return r;
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -296,14 +296,6 @@ __device__ __forceinline__ void stv(typename fvec<TN>::t v, __amdgpu_buffer_rsrc
                                            soff, AUX);
 }
 
-// max(x, floor) as one v_max_f32 (fmaxf adds a canonicalizing v_max per operand in IEEE mode);
-// floor is 0 (ReLU) or -inf (none); the accumulators hold no NaN of interest to quiet
-__device__ __forceinline__ float relu_floor(float x, float floor) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(floor), "v"(x));
-  return r;
-}
-
 template <int TM, int TN, int KC, int Q, int NW>
 __global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
   constexpr int OCT = 32 * TM;           // output channels of the block

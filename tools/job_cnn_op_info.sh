@@ -1,6 +1,7 @@
 #!/bin/bash
 # cnn_op_info on the GPU: its tests, then the conv-ops-1-5-20 and SGEMM eff tables against the
-# rocBLAS / MIOpen comparator (graph-amortized per-call times, as the bench), written under gpurun_out/
+# rocBLAS / MIOpen comparator (eff rows: both sides in the reference's per-call event convention, the
+# last of --run-iter calls; the graph-amortized per-call time of ours in the log), written under gpurun_out/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 B=boda-1_amd/bin/boda_hip_cnn_op_info
