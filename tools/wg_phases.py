@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--conv", action="append", default=[])
     ap.add_argument("--cfg", action="append", default=[])
     ap.add_argument("--splits", default="1")
+    ap.add_argument("--slowest", type=int, default=0, help="also print the N slowest blocks' phases")
     a = ap.parse_args()
     dev = boda_hip.Device(0)
     names = boda_hip.tune_cfg_names(1)
@@ -43,8 +44,21 @@ def main():
                 mx = max(r[7] for r in rows)
                 print("%s %s S=%d blocks=%d iters/blk %.1f | wait %.0f dma %.0f xf %.0f mfma %.0f epi %.0f "
                       "| total %.0f (max %.0f) cyc; per iter: wait %.0f dma %.0f xf %.0f mfma %.0f" % (
-                          c, cn, S, n, avg[6], avg[1], avg[2], avg[3], avg[4], avg[5], avg[7], mx,
-                          avg[1] / avg[6], avg[2] / avg[6], avg[3] / avg[6], avg[4] / avg[6]), flush=True)
+                          c, cn, S, n, avg[6], avg[1], avg[2], 0.0, avg[4], avg[5], avg[7], mx,
+                          avg[1] / avg[6], avg[2] / avg[6], 0.0, avg[4] / avg[6]), flush=True)
+                if a.slowest:
+                    tot = sorted(r[7] for r in rows)
+                    print("   total percentiles 10/50/90/99: %.0f %.0f %.0f %.0f" % tuple(
+                        tot[min(n - 1, int(q * n))] for q in (0.1, 0.5, 0.9, 0.99)))
+                    t0 = min(r[3] for r in rows)  # slot 3: the block's start (absolute)
+                    end = [r[3] - t0 + r[7] for r in rows]
+                    st = sorted(r[3] - t0 for r in rows)
+                    print("   start skew percentiles 50/90/max: %.0f %.0f %.0f; end max %.0f" % (
+                        st[n // 2], st[int(0.9 * n)], st[-1], max(end)))
+                    for b in sorted(range(n), key=lambda b: -end[b])[:a.slowest]:
+                        r = rows[b]
+                        print("   block %4d (xcd %d): start %.0f iters %.0f wait %.0f mfma %.0f epi %.0f total %.0f end %.0f" % (
+                            b, b % 8, r[3] - t0, r[6], r[1], r[4], r[5], r[7], end[b]))
         dev.tune_set(1, -1, 0)
         wl.free()
     dev.close()
