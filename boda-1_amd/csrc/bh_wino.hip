@@ -60,6 +60,7 @@ struct WgArgs {
   uint32_t ipt, ipt_m, ipt_s, ipb, total_it;
   int relu, wt;
   int ow2;                       // OW even: a tile row's two outputs go as one 8-B store
+  int sepc;                      // cut tiles summed by wg_combine_kernel after the grid (no last arriver)
 #ifdef BH_KTRACE
   unsigned long long *trace;
 #endif
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
                                                (uint32_t)((q * NT + tid) * 16), 0, AUX_SC1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (whole) return;
+    if (whole || p.sepc) return;  // (sepc: summed by wg_combine_kernel)
     const uint32_t b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -698,10 +699,116 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
 #endif
 }
 
+// wg_combine_kernel: the cut tiles of a stream-K wgp grid (p.sepc), summed after it. A last arriver
+// inside the grid (the form without sepc) reads the tile's 3-5 slabs and stores its whole output --
+// 64 dword stores per thread where OW is odd -- while its pieces' other CUs idle: ~31 k cycles against
+// ~7 k for a piece's own epilogue, the grid's tail (tools/wg_phases.py --slowest). Here a block of the
+// same thread layout takes one tile and QC of its 16 accumulator elements, sums the slabs in block
+// order (the last arriver's order: bitwise the same output) and stores them with the grid's epilogue
+// (bias, residual, ReLU, 8-B pairs where OW is even). Tiles inside one block's range are skipped.
+template <int NWO, int NWT>
+__global__ __launch_bounds__(64 * NWO * NWT) void wg_combine_kernel(WgArgs p) {
+  constexpr int NW = NWO * NWT, NT = 64 * NW, OCT = 32 * NWO, TT = 32 * NWT, NQ = 16, QC = 4;
+  const uint32_t t = blockIdx.x / (NQ / QC), q0 = (blockIdx.x % (NQ / QC)) * QC;
+  const uint32_t tb = t * p.ipt, b0 = tb / p.ipb, b1 = (tb + p.ipt - 1) / p.ipb;
+  if (b0 == b1) return;  // uniform: stored by the grid
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave % NWO, wtl = wave / NWO;
+  const int li = lane & 31, kh = lane >> 5;
+  uint32_t oc0, g0;
+  if (p.ocs) {
+    const uint32_t q = fdiv(t, p.ngr_m, p.ngr_s);
+    oc0 = q * OCT;
+    g0 = (t - q * p.ngr) * TT;
+  } else {
+    const uint32_t pt = fdiv(t, p.tm_m, p.tm_s);
+    oc0 = (t - pt * p.tiles_m) * OCT;
+    g0 = pt * TT;
+  }
+  const uint32_t tg = g0 + (uint32_t)(wtl * 32 + li);
+  const bool stv = tg < p.T;
+  const uint32_t tgc = stv ? tg : 0u;
+  const uint32_t img = fdiv(tgc, p.tpi_m, p.tpi_s), rem = tgc - img * p.TPI;
+  const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+  const bool sx1 = 2 * tx + 1 < p.OW, sy1 = 2 * ty + 1 < p.OH;
+  const uint32_t sob = img * p.OCOHW + 2 * ty * p.OW + 2 * tx;
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+  uint32_t oc[QC];
+  float bias[QC];
+#pragma unroll
+  for (int i = 0; i < QC; ++i) {
+    const uint32_t q = q0 + (uint32_t)i;
+    oc[i] = oc0 + (uint32_t)(wo * 32) + 8u * (q >> 2) + 4u * (uint32_t)kh + (q & 3u);
+    bias[i] = ld1(rsb, oob_unless(oc[i] < p.OC, oc[i] * 4u));
+  }
+  // slabs in groups of 4: all 16 loads in flight, one wait per group
+  f32x4v y[QC];
+#pragma unroll
+  for (int i = 0; i < QC; ++i) y[i] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t bg = b0; bg <= b1; bg += 4) {
+    f32x4v x[4][QC];
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const uint32_t b = bg + (uint32_t)sb;
+      const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+      const uint32_t base = (b * 2 + s2) * (uint32_t)(NQ * NT * 16);
+#pragma unroll
+      for (int i = 0; i < QC; ++i)
+        x[sb][i] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rall, oob_unless(b <= b1, base + (uint32_t)(((q0 + i) * NT + tid) * 16)),
+                                                  0, AUX_SC1));
+    }
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int i = 0; i < QC; ++i)
+        if (bg + (uint32_t)sb <= b1) y[i] += x[sb][i];  // block order = k order
+  }
+#pragma unroll
+  for (int i = 0; i < QC; ++i) {
+    const bool ok = stv & (oc[i] < p.OC);
+    const uint32_t o = sob + oc[i] * p.OHW;
+    if (p.ow2) {  // uniform; o even: both 8-B pieces aligned
+      const uint32_t off[2] = {oob_unless(ok, o * 4u), oob_unless(ok & sy1, (o + p.OW) * 4u)};
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float z0 = y[i][2 * e] + bias[i], z1 = y[i][2 * e + 1] + bias[i];
+        if (p.res) {
+          z0 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
+          z1 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 4, 0));
+        }
+        if (p.relu) {
+          z0 = z0 < 0.0f ? 0.0f : z0;
+          z1 = z1 < 0.0f ? 0.0f : z1;
+        }
+        const __attribute__((ext_vector_type(2))) uint32_t v = {__builtin_bit_cast(uint32_t, z0),
+                                                               __builtin_bit_cast(uint32_t, z1)};
+        if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, off[e], 0, AUX_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b64(v, rso, off[e], 0, AUX_OUT);
+      }
+    } else {
+      const uint32_t off[4] = {oob_unless(ok, o * 4u), oob_unless(ok & sx1, (o + 1) * 4u),
+                               oob_unless(ok & sy1, (o + p.OW) * 4u), oob_unless(ok & sx1 & sy1, (o + p.OW + 1) * 4u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float z = y[i][e] + bias[i];
+        if (p.res) z += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsr, off[e], 0, 0));
+        z = (p.relu && z < 0.0f) ? 0.0f : z;
+        wg_store1(p, rso, off[e], z);
+      }
+    }
+  }
+}
+
 template <int NWO, int NWT, int D, int V4, int SP, int IL, int DBG = 0>
 cfg_t wgp_cfg(const char *name) {
   cfg_t c{name, 32 * NWO, 32 * NWT, WCI, 64 * NWO * NWT, {}, 1};
   c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgp_kernel<NWO, NWT, D, V4, SP, IL, DBG>;
+  c.k[A_KVEC][B_DIRECT][1] = (kern_t)(void *)wg_combine_kernel<NWO, NWT>;
   c.dc = 4;
   c.dc_ky = 3;
   c.dc_kx = 3;
@@ -751,7 +858,9 @@ int launch_wino_pack(bh_ctx *ctx, const float *filts, float *u, uint32_t OC, uin
 
 // Launch a Winograd configuration: UNSUP unless a stride-1 3x3 conv with pad <= 1, IC % 4 == 0,
 // whose strips fit the configuration's slot. splits: 0 / 1..4 blocks per CU, iterations dealt
-// equally; 5..8: blocks per CU 1..4, whole tiles per block; + 10: OC tiles slowest.
+// equally; 5..8: blocks per CU 1..4, whole tiles per block; + 10: OC tiles slowest; + 20: the
+// stream-K modes' cut tiles summed by wg_combine_kernel (a second launch) instead of their last
+// arrivers.
 int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, const float *bias, const float *res,
               float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
               uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
@@ -813,7 +922,10 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
     return bh::fail(BH_ERR, "conv: Winograd LDS attribute");
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, (int)NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
-  // splits: + 10 = OC tile slowest
+  // splits: + 20 = cut tiles summed by wg_combine_kernel after the grid (stream-K modes); + 10 = OC
+  // tile slowest
+  p.sepc = splits >= 20 ? 1 : 0;
+  if (splits >= 20) splits -= 20;
   p.ocs = splits >= 10 ? 1 : 0;
   if (splits >= 10) splits -= 10;
   p.ngr = ngroups;
@@ -837,7 +949,12 @@ int launch_wg(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, cons
   p.trace = (unsigned long long *)ctx->stamps + 65536;
 #endif
   void *args[] = {&p};
-  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(NT), args, first, true, "conv_wino", lds);
+  if (whole) p.sepc = 0;  // no cut tiles
+  if (!p.sepc) return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(NT), args, first, true, "conv_wino", lds);
+  rc = bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(NT), args, first, false, "conv_wino", lds);
+  if (rc != BH_OK) return rc;
+  return bh::launch(ctx, (const void *)c.k[A_KVEC][B_DIRECT][1], dim3((uint32_t)ntile * 4u, 1, 1), dim3(NT), args,
+                    false, true, "conv_wino_combine");
 }
 
 }  // namespace bhk

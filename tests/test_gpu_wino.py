@@ -7,7 +7,8 @@ tile row and column, 6x6, 14x14, 28x28, 56x56), ragged output channels (not a mu
 128-channel tile, nor of 32), unpadded and non-square inputs, under every grid mode the tuner may
 pick (splits 0: stream-K at the occupancy's blocks per CU, 1 / 2 blocks per CU, 5: whole tiles per
 block; 11 / 15: the same with the OC tile slowest -- the ngr fastdiv branch of tile_of and another
-stream-K slab / ticket pattern). The result is an exact-fp32 Winograd sum, so it is checked against the double-accumulated
+stream-K slab / ticket pattern; 20 / 21 / 31: the stream-K modes with the cut tiles summed by
+wg_combine_kernel after the grid, bitwise equal to their last-arriver forms). The result is an exact-fp32 Winograd sum, so it is checked against the double-accumulated
 oracle with the tolerances of test_gpu_conv.py -- the same bar every direct route
 meets -- and element-wise within the 2e-3 the reference allows cuDNN's 3x3 Winograd
 (min_sig_mag_rel_diff, src/rtc_prof.cc:314-319). A rerun gives the same bits (cut tiles are
@@ -56,7 +57,8 @@ def test_wg_config(dev, cn):
     ran = 0
     try:
         for s in SHAPES:
-            for splits in (0, 1, 2, 5, 11, 15):
+            outs = {}
+            for splits in (0, 1, 2, 5, 11, 15, 20, 21, 31):
                 dev.tune_set(1, ci, splits)
                 try:
                     out = run_conv(dev, s)
@@ -67,6 +69,9 @@ def test_wg_config(dev, cn):
                 np.testing.assert_array_equal(run_conv(dev, s), out)
                 if splits == 0:
                     np.testing.assert_array_equal(run_conv(dev, s, packed=True), out)
+                outs[splits] = out
+                if splits >= 20:  # the separate combine kernel sums the same slabs in the same order
+                    np.testing.assert_array_equal(out, outs[splits - 20])
     finally:
         dev.tune_set(1, -1, 0)
     assert ran >= 8, "config %s ran on too few shapes" % cn

@@ -227,7 +227,7 @@ def main():
                         continue
                     if cn.startswith("wg"):  # Winograd 3x3: S = grid mode as stream-K; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 3 and s.sy == s.sx == 1 and s.py <= 1 and s.px <= 1:
-                            cand += [(ci, 1), (ci, 5), (ci, 11), (ci, 15)]  # one block per CU (256 AGPRs)
+                            cand += [(ci, 1), (ci, 5), (ci, 11), (ci, 15), (ci, 21), (ci, 31)]  # one block per CU (256 AGPRs); +20: combine kernel
                         continue
                     if cn.startswith("wx"):  # position-split Winograd (planned grid); UNSUP for other ops
                         r = 5 if cn.startswith("wx25") else 3
