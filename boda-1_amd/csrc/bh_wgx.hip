@@ -62,6 +62,7 @@ struct WxArgs {
   uint32_t *cnt;              // arrival tickets, one per unit
   int relu, wt;
   int vst;                    // OW % MO == 0 and out / res MO-float aligned: a tile row per store
+  int sepc;                   // stream-K: cut units summed by wx_combine_kernel after the grid
 #ifdef BH_KTRACE
   unsigned long long *trace;  // per-block device-clock marks (tools/ktrace.py)
 #endif
@@ -623,7 +624,7 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
       asm volatile("" ::: "memory");
     }
     if constexpr (SK) {
-      if (!whole) {
+      if (!whole && !(SK == 1 && p.sepc)) {  // (sepc: summed by wx_combine_kernel)
         // the unit's blocks b0 .. b1 (in block order); the last to arrive sums their partials
         // (SK 2: tail unit t's S = total_it parts are blocks ipb + (t - ipb) S ..)
         const uint32_t b0 = SK == 2 ? p.ipb + (t - p.ipb) * p.total_it : (t * ipt) / p.ipb;
@@ -708,11 +709,115 @@ __global__ __launch_bounds__(64 * NW, 2) void wgx_kernel(WxArgs p) {
   KT(4);
 }
 
+// wx_combine_kernel: the cut units of a stream-K wgx grid (p.sepc, SK 1), summed after it instead of
+// by their last arrivers (whose extra ~5-11 us of slab reads and stores end the grid while the
+// pieces' other CUs idle, profiles/r05/ktrace_streamk_routes.log). One block per (unit, exchange
+// round r), the grid's thread layout: thread tid sums element r of its (channel, tile) pair over the
+// unit's slabs in block order (the last arriver's order: bitwise the same output) and stores as
+// the grid's epilogue does.
+template <int MO, int R, int NW>
+__global__ __launch_bounds__(64 * NW) void wx_combine_kernel(WxArgs p) {
+  using G = wx_geom<MO, R, NW>;
+  constexpr int XNT = G::NT, OCT = G::OCT, ECH = G::ECH, NR = 16 / ECH, MM = MO * MO;
+  const uint32_t t = blockIdx.x / NR, r = blockIdx.x % NR;
+  const uint32_t ipt = p.ipt, b0 = (t * ipt) / p.ipb, b1 = (t * ipt + ipt - 1) / p.ipb;
+  if (b0 == b1) return;  // uniform: a whole unit, stored by the grid
+  const uint32_t tid = threadIdx.x;
+  const uint32_t rog = tid / (ECH * 64), rel = (tid / 64) % ECH, rlane = tid & 63u;
+  const uint32_t oct = fdiv(t, p.ngr_m, p.ngr_s), oc0 = oct * OCT, g0 = (t - oct * p.ngr) * XTT;
+  const uint32_t rtile = g0 + (rlane & 31u);
+  const bool tvalid = rtile < p.T;
+  uint32_t obase, oy0, ox0;
+  {
+    const uint32_t tg = tvalid ? rtile : 0u;
+    const uint32_t img = fdiv(tg, p.tpi_m, p.tpi_s), rem = tg - img * p.TPI;
+    const uint32_t ty = fdiv(rem, p.tw_m, p.tw_s), tx = rem - ty * p.TW;
+    oy0 = MO * ty;
+    ox0 = MO * tx;
+    obase = img * p.OCOHW + oy0 * p.OW + ox0;
+  }
+  const uint32_t ee = r * ECH + rel;
+  const uint32_t oc = oc0 + rog * 32u + 8u * (ee >> 2) + 4u * (rlane >> 5) + (ee & 3u);
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.out, p.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.out_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(p.bias, p.bias ? p.OC * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t rall = make_rsrc(p.ws, 0x7fffff00u);
+  const float bb = ld1(rsb, oob_unless(oc < p.OC, oc * 4u));
+  float ys[MM];
+#pragma unroll
+  for (int q = 0; q < MM; ++q) ys[q] = 0.0f;
+  // slabs in groups of 4, all their loads in flight
+  for (uint32_t bg = b0; bg <= b1; bg += 4) {
+    f32x4v x[4][MM / 4];
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const uint32_t b = bg + (uint32_t)sb;
+      const uint32_t s2 = (b == b0 && t != fdiv(b * p.ipb, p.ipt_m, p.ipt_s)) ? 1u : 0u;
+      const uint32_t base = (b * 2 + s2) * (uint32_t)(NR * XNT * MM * 4);
+#pragma unroll
+      for (int q = 0; q < MM / 4; ++q)
+        x[sb][q] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rall, oob_unless(b <= b1, base + ((r * XNT + tid) * MM + 4 * q) * 4), 0,
+                                                  AUX_SC1));
+    }
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+      if (bg + (uint32_t)sb <= b1) {  // block order = k order
+#pragma unroll
+        for (int q = 0; q < MM / 4; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ys[4 * q + c] += x[sb][q][c];
+      }
+  }
+  const bool ok = tvalid & (oc < p.OC);
+  const uint32_t ob = obase + oc * p.OHW;
+#pragma unroll
+  for (int yy = 0; yy < MO; ++yy) {
+    if (p.vst) {  // uniform: OW % MO == 0 and MO-float aligned tensors -- a tile row is one store
+      typedef __attribute__((ext_vector_type(MO))) uint32_t uv_t;
+      typedef __attribute__((ext_vector_type(MO))) float fv_t;
+      const uint32_t off = oob_unless(ok & (oy0 + yy < p.OH), (ob + yy * p.OW) * 4u);
+      fv_t rv = {};
+      if (p.res) {
+        if constexpr (MO == 4) rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b128(rsr, off, 0, 0));
+        else rv = __builtin_bit_cast(fv_t, __builtin_amdgcn_raw_buffer_load_b64(rsr, off, 0, 0));
+      }
+      fv_t zv;
+#pragma unroll
+      for (int x = 0; x < MO; ++x) {
+        float z = ys[yy * MO + x] + bb;
+        if (p.res) z += rv[x];
+        zv[x] = (p.relu && z < 0.0f) ? 0.0f : z;
+      }
+      const uv_t v = __builtin_bit_cast(uv_t, zv);
+      if constexpr (MO == 4) {
+        if (p.wt) __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b128(v, rso, off, 0, AUX_OUT);
+      } else {
+        if (p.wt) __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_SC1);
+        else __builtin_amdgcn_raw_buffer_store_b64(v, rso, off, 0, AUX_OUT);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int x = 0; x < MO; ++x) {
+      const bool in = ok & (oy0 + yy < p.OH) & (ox0 + x < p.OW);
+      const uint32_t off = oob_unless(in, (ob + yy * p.OW + x) * 4u);
+      float z = ys[yy * MO + x] + bb;
+      if (p.res) z += ld1(rsr, off);
+      z = (p.relu && z < 0.0f) ? 0.0f : z;
+      if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_SC1);
+      else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z), rso, off, 0, AUX_OUT);
+    }
+  }
+}
+
 template <int MO, int R, int SP, int NW, int DBG = 0, int SK = 0>
 cfg_t wgx_cfg(const char *name) {
   using G = wx_geom<MO, R, NW>;
   cfg_t c{name, G::OCT, XTT, XC, G::NT, {}, 1};
   c.k[A_KVEC][B_DIRECT][0] = (kern_t)(void *)wgx_kernel<MO, R, SP, NW, SK, DBG>;
+  if constexpr (SK == 1) c.k[A_KVEC][B_DIRECT][1] = (kern_t)(void *)wx_combine_kernel<MO, R, NW>;
   c.dc_wpm = SK;  // (dc == 5) 1: persistent stream-K grid, 2 / 3: whole units + a split tail
   c.dc = 5;
   c.dc_ky = R;
@@ -846,7 +951,6 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
                float *out, uint32_t out_ctot, uint32_t B, uint32_t IC, uint32_t H, uint32_t W, uint32_t OC, uint32_t KY,
                uint32_t KX, uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int relu, int wt, uint32_t splits,
                bool first) {
-  (void)splits;
   const uint32_t R = (uint32_t)c.dc_ky, MO = (uint32_t)c.dc_s, N = MO + R - 1;
   if (KY != R || KX != R || sy != 1 || sx != 1 || py != px || py > R / 2)
     return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for stride-1 square-padded convs of its kernel size");
@@ -978,7 +1082,14 @@ int launch_wgx(bh_ctx *ctx, const cfg_t &c, const float *u, const float *in, con
   p.trace = (unsigned long long *)ctx->stamps + 65536;
 #endif
   void *args[] = {&p};
-  return bh::launch(ctx, k, dim3(G, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
+  // splits 20 on a stream-K configuration: the cut units summed by wx_combine_kernel (a second launch)
+  p.sepc = (c.dc_wpm == 1 && splits == 20) ? 1 : 0;
+  if (!p.sepc) return bh::launch(ctx, k, dim3(G, 1, 1), dim3(XNT), args, first, true, "conv_wgx", lds);
+  int rc = bh::launch(ctx, k, dim3(G, 1, 1), dim3(XNT), args, first, false, "conv_wgx", lds);
+  if (rc != BH_OK) return rc;
+  const uint32_t NR = 16 / (XNT / ((XNT / 64 / NPG) * 64));
+  return bh::launch(ctx, (const void *)c.k[A_KVEC][B_DIRECT][1], dim3((uint32_t)units * NR, 1, 1), dim3(XNT), args,
+                    false, true, "conv_wgx_combine");
 }
 
 }  // namespace bhk

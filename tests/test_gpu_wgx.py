@@ -86,6 +86,29 @@ def test_wx_config(dev, cn):
     assert ran >= 3, "config %s ran on too few shapes" % cn
 
 
+@pytest.mark.parametrize("cn", [n for n in WX if n.endswith("k")])
+def test_wx_combine_kernel(dev, cn):
+    """Stream-K (SK 1) configurations with splits 20: the cut units summed by wx_combine_kernel after
+    the grid -- the same slabs in the same block order as the last arriver, so the same bits."""
+    ci = boda_hip.tune_cfg_names(1).index(cn)
+    ran = 0
+    try:
+        for s in shapes_of(cn):
+            dev.tune_set(1, ci, 0)
+            try:
+                out = run_conv(dev, s)
+            except boda_hip.UnsupportedError:
+                continue
+            dev.tune_set(1, ci, 20)
+            sep = run_conv(dev, s)
+            check(sep, s)
+            np.testing.assert_array_equal(sep, out)
+            ran += 1
+    finally:
+        dev.tune_set(1, -1, 0)
+    assert ran >= 3, "config %s ran on too few shapes" % cn
+
+
 @pytest.mark.parametrize("cn", WX)
 def test_wx_rejects_other_shapes(dev, cn):
     dev.tune_set(1, boda_hip.tune_cfg_names(1).index(cn), 0)

@@ -233,6 +233,8 @@ def main():
                         r = 5 if cn.startswith("wx25") else 3
                         if kind == 1 and s.KY == s.KX == r and s.sy == s.sx == 1 and s.py == s.px <= r // 2:
                             cand.append((ci, 0))
+                            if cn.endswith("k"):  # stream-K: + the separate combine kernel (splits 20)
+                                cand.append((ci, 20))
                         continue
                     if cn.startswith(("ks", "kn")):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 1 and s.sy == s.sx == 1 and s.py == s.px == 0:
