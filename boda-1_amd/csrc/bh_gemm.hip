@@ -1226,7 +1226,7 @@ int launch_conv(bh_ctx *ctx, const float *in, const float *filts, const float *p
                                   std::to_string(fc_c.BN) + " with K % 4 == 0");
       if (fc && avec) {
         void *args[] = {&p};
-        return bh::launch(ctx, (const void *)fc_c.k[A_MVEC][B_FC][0], dim3((OC + fc_c.BM - 1) / fc_c.BM), dim3(256),
+        return bh::launch(ctx, (const void *)fc_c.k[A_MVEC][B_FC][0], dim3((OC + fc_c.BM - 1) / fc_c.BM), dim3(fc_c.NT),
                           args, first, true, "conv");
       }
       tile_fallback = true;  // 16-B loads of the bank or the input rows impossible
