@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 5: the Winograd (wgp / wgi) cut-tile combine with double-buffered slab loads: parity, per-phase
-# clocks, then a same-box A B A B of the conv set against the previous build (B = libboda_hip_prev.so)
+# clocks, then a same-box A B A B of the conv set against the previous build (B = libboda_hip_prev.so:
+# bh_wino.hip of the parent commit compiled into build/bh_wino_prev.o and linked with the other objects
+# as boda-1_amd/Makefile links libboda_hip.so); profiles/r05/wg_combine/ab_shared_*
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 tools/gpu_job.sh \
