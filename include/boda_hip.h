@@ -282,7 +282,10 @@ int bh_variant_name_ctx(bh_ctx *ctx, int op, const uint32_t *dims, char *buf, si
 /* force tile configuration cfg_index (-1: back to table/heuristic) and K splits
  * for every later call of op on this context: splits 0 = planned, n > 0 = n
  * splits combined in-kernel by each tile's last-arriving block, -n = n splits
- * combined by a separate reduce kernel. Both combines sum in a fixed order. */
+ * combined by a separate reduce kernel. Both combines sum in a fixed order.
+ * Configuration families reuse splits as their grid mode (direct / Winograd
+ * kernels: blocks per CU, whole tiles, + 10 OC tile slowest, + 20 a stream-K
+ * grid's cut tiles summed by a second combine kernel). */
 int bh_tune_set(bh_ctx *ctx, int op, int cfg_index, int splits);
 /* force the output store policy of every later call of op on this context: wt 1 = the outputs
  * are written through (sc1) during the kernel instead of left dirty in L2 for the next kernel
