@@ -79,6 +79,20 @@ def shard_units(shapes, tags, world, rank):
     return units, [units[i] for i in parts[rank]], pred
 
 
+def build_hash():
+    """sha256 over the kernel sources and the tuning table: what decides which kernel runs each unit
+    and how fast (a committed rocprof figure is reported only for the build it was measured on)."""
+    import hashlib
+    h = hashlib.sha256()
+    src = os.path.join(ROOT, "boda-1_amd", "csrc")
+    for fn in sorted(os.listdir(src)):
+        if fn.endswith((".hip", ".h")):
+            h.update(fn.encode())
+            h.update(open(os.path.join(src, fn), "rb").read())
+    h.update(open(os.path.join(ROOT, "boda-1_amd", "tuning", "gfx950.tune"), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def cpu_info():
     """Host facts for the CPU baseline line: logical CPUs, the CPUs this process may run on, the
     CPU model string."""
@@ -332,7 +346,12 @@ def main():
     if os.path.exists(rp):
         try:
             rj = json.load(open(rp))
-            if rj.get("kernel") == dom and rj.get("avg_ns"):
+            units = sorted(r["dims"] for r in recs if r["variant"] == dom)
+            same = rj.get("units") == units and rj.get("build_hash") == build_hash()
+            if rj.get("kernel") == dom and rj.get("avg_ns") and not same:
+                roof["frac_rocprof_stale"] = ("profiles/rocprof_dominant.json was measured on another build or "
+                                              "other launches of this kernel: not reported")
+            if rj.get("kernel") == dom and rj.get("avg_ns") and same:
                 a_rp = roof["avg_flops_per_launch"] / (rj["avg_ns"] * 1e-9)
                 roof["avg_launch_ms_rocprof"] = round(rj["avg_ns"] * 1e-6, 4)
                 roof["frac_rocprof"] = round(a_rp / runner.PEAK_FP32_FLOPS, 4)

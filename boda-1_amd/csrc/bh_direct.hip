@@ -624,7 +624,7 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   float biasr[TM];
 #pragma unroll
   for (int t = 0; t < TM; ++t) biasr[t] = bres[32 * t + li];
-  const float floor0 = p.relu ? 0.0f : -__builtin_inff();
+  const float floor0 = p.relu ? 0.0f : __builtin_nanf("");  // relu_floor: NaN = no clamp
   bool pending = false;
   int slot = 0;
   uint32_t g = 0;

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
   // (4 kh rows) goes into its VGPR offset, the rest of the row into the scalar soffset
   // the epilogue's wave-uniform choices (mask, residual, store policy) are taken once per unit:
   // branches per row cost a basic block per store
-  const float floor0 = p.relu ? 0.0f : -__builtin_inff();
+  const float floor0 = p.relu ? 0.0f : __builtin_nanf("");  // relu_floor: NaN = no clamp
   auto epilogue = [&](auto masked, auto res, auto wt) {
     // the rows' scalar offsets are made here, per unit (laundered stride: hoisted out of the unit
     // loop, 16 TM of them spilled SGPRs into VGPR lanes)

@@ -182,7 +182,7 @@ int main(int argc, char **argv) {
   if (o.kv.count("pp-vals")) {  // GPU-free check of the number formatting: pp_val of a comma list
     std::stringstream ss(o.get("pp-vals"));
     std::string t;
-    while (std::getline(ss, t, ',')) std::cout << pp_val(std::stod(t)) << "\n";
+    while (std::getline(ss, t, ',')) std::cout << pp_val(parse_f64(t, "value")) << "\n";
     return 0;
   }
   if (o.get("cnn-func-sigs-fn").empty()) {
@@ -202,25 +202,25 @@ int main(int argc, char **argv) {
     }
     if (!o.get("op-info-tab-fn").empty()) oit.open(o.get("op-info-tab-fn"));
     if (!o.get("op-eff-tab-fn").empty()) oet.open(o.get("op-eff-tab-fn"));
-    const uint32_t print_format = std::stoul(o.get("print-format", "0"));
+    const uint32_t print_format = parse_u32(o.get("print-format", "0"), "--print-format");
     const bool inc_info = o.get("inc-op-info-in-eff", "0") != "0";
     // not in the reference (its conv eff rows drop the comparator's time, latex-util.H:90-97)
     const bool eff_comp = o.get("eff-comp", "0") != "0";
-    const double peak = std::stod(o.get("peak-flops", std::to_string(PEAK_FP32_FLOPS)));
-    const uint32_t run_iter = std::max(1ul, std::stoul(o.get("run-iter", "1")));
-    const uint32_t graph_reps = std::stoul(o.get("graph-reps", "0"));
-    const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
-    const double toler = std::stod(o.get("mrd-toler", "2e-4"));
+    const double peak = parse_f64(o.get("peak-flops", std::to_string(PEAK_FP32_FLOPS)), "--peak-flops");
+    const uint32_t run_iter = std::max(1u, parse_u32(o.get("run-iter", "1"), "--run-iter"));
+    const uint32_t graph_reps = parse_u32(o.get("graph-reps", "0"), "--graph-reps");
+    const uint32_t mode = parse_u32(o.get("gen-data-mode", "5"), "--gen-data-mode");
+    const double toler = parse_f64(o.get("mrd-toler", "2e-4"), "--mrd-toler");
     // Winograd routes (variant names *_wino_*) compare at the reference's Winograd tolerance, 2e-3
     // (ops-prof's widening for cuDNN's 3x3 Winograd, src/rtc_prof.cc:314-319): the input / output
     // transforms turn cancellation in the direct sum into element errors min_sig_mag_rel_diff sees
     // on near-zero outputs (measured per op with --show-mrd=1)
-    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-3"));
+    const double wino_toler = parse_f64(o.get("wino-mrd-toler", "2e-3"), "--wino-mrd-toler");
     const bool show_mrd = o.get("show-mrd", "0") != "0";
-    const uint32_t max_err = std::stoul(o.get("max-err", "10"));
+    const uint32_t max_err = parse_u32(o.get("max-err", "10"), "--max-err");
     const std::string comp = o.get("comp", "vendor");
     if (comp != "vendor" && comp != "none") rt_err("--comp must be vendor or none");
-    const int device = std::stoi(o.get("device", "0"));
+    const int device = parse_i32(o.get("device", "0"), "--device");
     // --no-run: rows only, no device (runtimes NAN, as a failed profile call leaves them, cnn-prof.cc:95)
     const bool no_run = o.get("no-run", "0") != "0";
 

@@ -225,13 +225,13 @@ struct hip_compute_t : public rtc_compute_t {
       };
       if (std::string const *n = sv("hip_cfg")) {
         std::string const *sp = sv("hip_splits");
-        bh_check(bh_tune_set(ctx, op, cfg_index_of(op, *n), sp ? std::stoi(*sp) : 0), "bh_tune_set");
+        bh_check(bh_tune_set(ctx, op, cfg_index_of(op, *n), sp ? parse_i32(*sp, "splits") : 0), "bh_tune_set");
         cfg = true;
       } else if (sv("hip_splits")) {
         rt_err("op_tune: splits without cfg");
       }
       if (std::string const *w = sv("hip_wt")) {
-        bh_check(bh_tune_set_policy(ctx, op, std::stoi(*w)), "bh_tune_set_policy");
+        bh_check(bh_tune_set_policy(ctx, op, parse_i32(*w, "wt")), "bh_tune_set_policy");
         wt = true;
       }
     }
@@ -244,7 +244,7 @@ struct hip_compute_t : public rtc_compute_t {
   // default: every bank of the kernel size, bh_conv_filts_pack's layout)
   static uint32_t pack_banks_of(op_base_t const &op) {
     auto it = op.str_vals.find("hip_pack_banks");
-    return it == op.str_vals.end() ? BH_BANKS_ALL : (uint32_t)std::stoul(it->second);
+    return it == op.str_vals.end() ? BH_BANKS_ALL : parse_u32(it->second, "bank mask");
   }
   std::string variant_of(int op, uint32_t const *d) {
     char buf[192];

@@ -171,7 +171,7 @@ std::string nda_digest_t::to_hex() const {
 nda_digest_t nda_digest_t::from_hex(std::string const &h) {
   if (h.size() % 2) rt_err("digest hex: odd length");
   std::string b;
-  for (size_t i = 0; i < h.size(); i += 2) b += (char)std::stoul(h.substr(i, 2), nullptr, 16);
+  for (size_t i = 0; i < h.size(); i += 2) b += (char)parse_u32(h.substr(i, 2), "hex byte", 16);
   br_t r(b);
   if (r.raw<uint8_t>() != 1) rt_err("digest hex: null digest");
   std::string tn = r.str();
@@ -235,7 +235,7 @@ bool read_next_wisdom(std::istream &in, op_wisdom_t &w) {
         if (l != "op_run_t") rt_err("wisdom: unknown op_tune_wisdom_t command '" + l + "'");
         op_run_t r;
         r.plat_tag = must_getline(in);
-        r.rt_secs = std::stod(must_getline(in));
+        r.rt_secs = parse_f64(must_getline(in), "run time");
         r.err = must_getline(in);
         if (r.err.empty()) r.op_line = must_getline(in);
         t.second.push_back(r);

@@ -26,7 +26,7 @@ dims_t dims_from_lexp(lexp_t const &l, std::string const &tn) {
       continue;
     }
     if (k.second->is_list) rt_err("nested list where a dimension size was expected");
-    nd.emplace_back(k.first, (uint32_t)std::stoul(k.second->leaf));
+    nd.emplace_back(k.first, parse_u32(k.second->leaf, "dim size"));
   }
   return dims_t(nd, t);
 }
@@ -53,7 +53,7 @@ op_base_t parse_op_line(std::string const &line) {
         p_lexp_t tn = n.find("tn"), dims = n.find("dims"), v = n.find("v");
         std::string tns = tn ? tn->leaf : "float";
         if (dims) op.dims_vals[k.first] = dims_from_lexp(*dims, tns);
-        else if (v) op.scalars[k.first] = std::stoull(v->leaf);
+        else if (v) op.scalars[k.first] = parse_u64(v->leaf, "scalar " + k.first);
         else rt_err("nda '" + k.first + "' has neither dims nor v");
       }
     return op;
@@ -69,7 +69,7 @@ op_base_t parse_op_line(std::string const &line) {
       for (auto const &s : k.second->kids) {
         std::string const &v = s.second->leaf;
         bool num = !v.empty() && std::all_of(v.begin(), v.end(), ::isdigit);
-        if (num) op.scalars[s.first] = std::stoull(v);
+        if (num) op.scalars[s.first] = parse_u64(v, "scalar " + s.first);
         else op.str_vals[s.first] = v;
       }
     } else {
@@ -199,8 +199,8 @@ hip_op_tune_t parse_hip_op_tune(std::string const &s) {
     try {
       if (kv.first == "use_be") t.use_be = v;
       else if (kv.first == "cfg") t.cfg = v;
-      else if (kv.first == "splits") t.splits = std::stoi(v);
-      else if (kv.first == "wt") t.wt = std::stoi(v);
+      else if (kv.first == "splits") t.splits = parse_i32(v, "splits");
+      else if (kv.first == "wt") t.wt = parse_i32(v, "wt");
       else rt_err("op_tune: unknown field '" + kv.first + "' (use_be, cfg, splits, wt)");
     } catch (std::logic_error const &) {
       rt_err("op_tune: bad value '" + v + "' for " + kv.first);

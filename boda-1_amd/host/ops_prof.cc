@@ -87,7 +87,7 @@ bool same_op(op_base_t const &a, op_base_t const &b) {
 std::vector<bool> lpt_mine(std::vector<std::string> const &lines, std::string const &spec) {
   size_t sl = spec.find('/');
   if (sl == std::string::npos) rt_err("--shard wants k/n");
-  uint32_t k = std::stoul(spec.substr(0, sl)), n = std::stoul(spec.substr(sl + 1));
+  uint32_t k = parse_u32(spec.substr(0, sl), "shard index"), n = parse_u32(spec.substr(sl + 1), "shard count");
   if (!n || k >= n) rt_err("--shard: need 0 <= k < n");
   std::vector<std::pair<double, size_t>> cost;
   for (size_t i = 0; i < lines.size(); ++i) {
@@ -177,13 +177,13 @@ int main(int argc, char **argv) {
                    "  [--skip-ops=0] [--shard=k/n] | --selftest-wisdom=F | --dump-ops=F | --list-shard=k/n --ops-fn=F\n";
       return 2;
     }
-    const uint32_t mode = std::stoul(o.get("gen-data-mode", "5"));
-    const uint32_t run_iter = std::max(1ul, std::stoul(o.get("run-iter", "1")));
-    const double mrd = std::stod(o.get("mrd-toler", "2e-4"));
-    const uint32_t max_err = std::stoul(o.get("max-err", "10"));
+    const uint32_t mode = parse_u32(o.get("gen-data-mode", "5"), "--gen-data-mode");
+    const uint32_t run_iter = std::max(1u, parse_u32(o.get("run-iter", "1"), "--run-iter"));
+    const double mrd = parse_f64(o.get("mrd-toler", "2e-4"), "--mrd-toler");
+    const uint32_t max_err = parse_u32(o.get("max-err", "10"), "--max-err");
     const bool write_runs = o.get("write-runs", "0") != "0";
     const bool write_kg_digest = o.get("write-kg-digest", "1") != "0";
-    uint32_t skip = std::stoul(o.get("skip-ops", "0"));
+    uint32_t skip = parse_u32(o.get("skip-ops", "0"), "--skip-ops");
     // --op-tunes (a tag -> op_tune map, iterated in tag order as the reference's map_str_op_tune_t)
     // and --kg-tune-tag (src/rtc_prof.cc:151,166): the kg tune runs first; its outputs are the lhs
     // of a full-data comp_vars against every tune, itself included (:276-321)
@@ -211,16 +211,16 @@ int main(int argc, char **argv) {
     std::map<std::string, double> func_toler;
     {
       p_lexp_t l = parse_lexp(o.get("func-mrd-toler", "()"));
-      for (auto const &kv : l->kids) func_toler[kv.first] = std::stod(kv.second->leaf);
+      for (auto const &kv : l->kids) func_toler[kv.first] = parse_f64(kv.second->leaf, "tolerance");
     }
     // Winograd routes widen to 2e-3, the reference's widening for cuDNN's 3x3 Winograd
     // (src/rtc_prof.cc:314-319), unless --func-mrd-toler names them
-    const double wino_toler = std::stod(o.get("wino-mrd-toler", "2e-3"));
+    const double wino_toler = parse_f64(o.get("wino-mrd-toler", "2e-3"), "--wino-mrd-toler");
     // --live-mrd-toler (MI355X extension, default 0: the reference's single tolerance): a floor for
     // the full-data compare only, the digest compare keeps the function's tolerance. Two fp32
     // routes summing K in different orders differ element-wise by about their error against the
     // exact sum, far above a digest's 2e-4 at K in the thousands
-    const double live_floor = std::stod(o.get("live-mrd-toler", "0"));
+    const double live_floor = parse_f64(o.get("live-mrd-toler", "0"), "--live-mrd-toler");
     auto toler_of = [&](std::string const &variant) {
       double t = mrd;
       size_t best = 0;
@@ -251,7 +251,7 @@ int main(int argc, char **argv) {
     std::vector<bool> mine(lines.size(), true);
     if (!o.get("shard").empty()) mine = lpt_mine(lines, o.get("shard"));
 
-    p_rtc_compute_t rtc = make_hip_compute(std::stoi(o.get("device", "0")));
+    p_rtc_compute_t rtc = make_hip_compute(parse_i32(o.get("device", "0"), "--device"));
     rtc->init();
     const std::string plat = rtc->get_plat_tag();
     uint32_t num_mad_fail = 0, n_unsup = 0;

@@ -38,8 +38,8 @@ int main(int argc, char **argv) {
     std::stringstream ss;
     ss << pf.rdbuf();
     const std::string fn = kv.count("func-name") ? kv["func-name"] : "my_dot";
-    const uint32_t n = kv.count("data-sz") ? (uint32_t)std::stoul(kv["data-sz"]) : 10000u;
-    p_rtc_compute_t rtc = make_hip_compute(kv.count("device") ? std::stoi(kv["device"]) : 0);
+    const uint32_t n = kv.count("data-sz") ? parse_u32(kv["data-sz"], "data-sz") : 10000u;
+    p_rtc_compute_t rtc = make_hip_compute(kv.count("device") ? parse_i32(kv["device"], "device") : 0);
     rtc->init();
     op_base_t dot;
     dot.func_name = fn;

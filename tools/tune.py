@@ -125,10 +125,40 @@ def time_op_flush(dev, wl, i, reps):
     return statistics.median(out)
 
 
+def pick_route(med, err, prev, rejected, min_gain):
+    """The route a confirmed sweep writes for one op.
+
+    med: {(cfg, splits): median ms}, ("default", 0) = the heuristic route (table off); err: {(cfg,
+    splits): element error vs the oracle} (min_sig_mag_rel_diff(1), routes without a measurement absent);
+    prev: the --out table's route or None; rejected: routes over their accuracy gate (never chosen).
+    Returns (cfg, splits) or None = no table entry (the default route is at least as good).
+      * the fastest admissible route, but the previous table route stays unless beaten by min_gain;
+      * among the routes within min_gain of that pick, the most accurate one (an element error
+        measured lower by at least 2x) -- two routes that time alike should not differ 3x in error
+        (VERDICT r05: dm3 at 6e-4 where gvs gives 2e-4 on the same op);
+      * a previous route that is rejected never survives, and when the default wins the op gets no
+        entry (write_table then DELETES a merged table's old line)."""
+    ok = {r: t for r, t in med.items() if r not in rejected}
+    if not ok:
+        return None
+    r_best = min(ok, key=lambda r: ok[r])
+    t_best = ok[r_best]
+    if prev is not None and prev in ok and prev != r_best and t_best >= (1 - min_gain) * ok[prev]:
+        r_best, t_best = prev, ok[prev]
+    e_best = err.get(r_best)
+    if e_best is not None:
+        near = [r for r, t in ok.items() if t <= t_best / (1 - min_gain) and r in err and 2 * err[r] <= e_best]
+        if near:
+            r_best = min(near, key=lambda r: (err[r], ok[r]))
+    return None if r_best[0] == "default" else r_best
+
+
 def write_table(args, plat, table, results):
+    """table: {key: (cfg, splits, ms, default ms, wt)}, or {key: None} = the op must have no entry
+    (with --merge its old line is removed)."""
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    lines = {k: "%s cfg=%s splits=%d red=%s%s" % (k, cn, abs(S), "k" if S < 0 else "i", " wt=1" if wt else "")
-             for k, (cn, S, t, td, wt) in table.items()}
+    lines = {k: "%s cfg=%s splits=%d red=%s%s" % (k, v[0], abs(v[1]), "k" if v[1] < 0 else "i", " wt=1" if v[4] else "")
+             for k, v in table.items() if v is not None}
     if args.merge and os.path.exists(args.out):
         old = {}
         for l in open(args.out):
@@ -136,6 +166,9 @@ def write_table(args, plat, table, results):
                 continue
             old[l[:l.index(" cfg=")]] = l.rstrip("\n")
         old.update(lines)
+        for k, v in table.items():
+            if v is None:
+                old.pop(k, None)
         lines = old
     tmp = args.out + ".tmp"
     with open(tmp, "w") as f:
@@ -299,19 +332,23 @@ def main():
                 # slower than it is never written
                 dev.tune_set(kind, -1, 0)
                 med = {("default", 0): statistics.median(time_op(dev, wl, 0, args.reps) for _ in range(args.confirm))}
+                errs = {}
+                if kind == 1:  # every finalist's element error (the most accurate of near-equal routes wins)
+                    errs[("default", 0)] = wino_error(wl, s)
                 for cn, S in fin:
                     dev.tune_set(kind, names[kind].index(cn), S)
                     try:
                         med[(cn, S)] = statistics.median(time_op(dev, wl, 0, args.reps) for _ in range(args.confirm))
+                        if kind == 1:
+                            errs[(cn, S)] = wino_error(wl, s)
                     except boda_hip.UnsupportedError:
                         pass
                 dev.tune_set(kind, -1, 0)
                 for (cn, S), t in med.items():
-                    results.append({"key": key, "cfg": cn, "splits": S, "ms": t, "confirm": args.confirm})
-                (cn, S), t = min(med.items(), key=lambda kv: kv[1])
-                best = (t, -1, 0) if cn == "default" else (t, names[kind].index(cn), S)
-                if key in prev and prev[key] in med and t >= (1 - args.min_gain) * med[prev[key]]:
-                    best = (med[prev[key]], names[kind].index(prev[key][0]), prev[key][1])
+                    results.append({"key": key, "cfg": cn, "splits": S, "ms": t, "confirm": args.confirm,
+                                    "err": errs.get((cn, S))})
+                pick = pick_route(med, errs, prev.get(key), rejected, args.min_gain)
+                best = (t_def, -1, 0) if pick is None else (med[pick], names[kind].index(pick[0]), pick[1])
             elif key in prev and prev[key] not in rejected:  # keep the table's choice unless clearly beaten
                 pt = [x["ms"] for x in results if x["key"] == key and x["cfg"] == prev[key][0]
                       and x["splits"] == prev[key][1]]
@@ -335,8 +372,9 @@ def main():
                 dev.tune_set_policy(kind, -1)
                 dev.tune_set(kind, -1, 0)
             wl.free()
-            if best[1] >= 0:
-                table[key] = (names[kind][best[1]], best[2], best[0], t_def, wt)
+            # no route beats the default (or the previous entry was rejected): no entry, and a merged
+            # table's old line for the op is deleted
+            table[key] = (names[kind][best[1]], best[2], best[0], t_def, wt) if best[1] >= 0 else None
             rf = runner.roofline_secs(s) * 1e3
             print("%-48s default %.4f ms  best %s S=%+d %.4f ms  roofline %.4f ms (%.0f%%)" % (
                 key, t_def, names[kind][best[1]] if best[1] >= 0 else "default", best[2], best[0], rf,
@@ -344,7 +382,9 @@ def main():
             if args.merge:  # written after every op: a sweep cut short by a time limit keeps its progress
                 write_table(args, plat, table, results)
     write_table(args, plat, table, results)
-    print("wrote %d entries to %s in %.0f s" % (len(table), args.out, time.time() - t_start))
+    print("wrote %d entries (%d deletions) to %s in %.0f s" % (sum(v is not None for v in table.values()),
+                                                          sum(v is None for v in table.values()), args.out,
+                                                          time.time() - t_start))
     dev.close()
 
 
