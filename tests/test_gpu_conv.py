@@ -25,6 +25,11 @@ pytestmark = pytest.mark.gpu
 
 NORM_TOL, RL2_TOL = 1e-4, 1e-5
 WINO_ELEM_TOL = 2e-3  # src/rtc_prof.cc:314-319
+# Every other route, element-wise: 1e-3 = 5x Boda's default ops-prof tolerance (2e-4, src/rtc_prof.cc:160),
+# which bounds a digest of the output, not each element; the direct routes' worst measured element
+# error on the 3x3 table ops is 6.4e-4 (dm3w16x64c8, profiles/r05/route_acc_3x3.txt), the fp32 sum of
+# K ~ 10^3 products against a double-accumulated oracle
+DIRECT_ELEM_TOL = 1e-3
 # conv-full-gen5 op 178 == ops-prof-conv-3x3-cudnn-boda op 37 (same op, same stored digest)
 KNOWN_REF_DIGEST_OUTLIERS = {ops.ConvShape(5, 384, 13, 13, 384, 3, 3, 1, 1, 1, 1)}
 
@@ -59,14 +64,18 @@ def is_wino(variant):
 
 
 def check_vs_oracle(out, s, mode=5, relu=1, with_bias=True, variant=None):
-    """The normalized bars; with variant (the route that ran) a Winograd route's element bar too."""
+    """The normalized bars and the element bar of the route that ran (Winograd: 2e-3, others 1e-3;
+    variant None: the route of a call made with an override, checked as a direct route)."""
     inp, filts, biases = orc.gen_conv(s, mode)
     ref = orc.conv_ref(inp, filts, biases if with_bias else None, s, relu)
     nm, rl2, hyb = orc.normalized_errors(ref, out)
     assert nm <= NORM_TOL and rl2 <= RL2_TOL, (s, nm, rl2, hyb)
-    if variant is not None and is_wino(variant):
-        assert hyb <= WINO_ELEM_TOL, (s, variant, hyb)
+    assert hyb <= elem_tol(variant), (s, variant, hyb)
     return hyb
+
+
+def elem_tol(variant):
+    return WINO_ELEM_TOL if variant is not None and is_wino(variant) else DIRECT_ELEM_TOL
 
 
 def test_gen_data_matches_oracle(dev):

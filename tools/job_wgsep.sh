@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: stream-K Winograd cut tiles summed by a separate combine kernel (grid modes + 20): Winograd
 # parity (every wg config and grid mode, the table's routes), per-phase clocks, then a same-box
-# A B A B of the conv set and op_sigs, table without (A = tools/prev.tune) and with (B) the + 20 routes
+# A B A B of the conv set and op_sigs, table without (A = profiles/r05/tables/prev.tune) and with (B) the + 20 routes
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 tools/gpu_job.sh \
