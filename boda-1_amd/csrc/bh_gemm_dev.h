@@ -372,6 +372,7 @@ struct cfg_t {
   int fcv = 0;        // gv: batch-streaming ipconv kernel (bh_gv.hip fcv_kernel), batch <= BN
   int ref64 = 0;      // double-accumulating known-good kernel (bh_ref64.hip), never tuned in
   int k1n = 0;        // dc == 3: the pixels-on-N form (bh_k1s.hip k1n_kernel; gv_cx pixels per lane)
+  int k1d = 0;        // dc == 3: the whole bank resident, input by 16-B LDS-DMA (bh_k1s.hip k1d_kernel)
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and

@@ -505,6 +505,231 @@ __global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
   vm_wait<0>();
 }
 
+// k1d_kernel (round 6, configs kd<OCT>c<KC>d<D>w<NW>): the pixels-on-N form with the input staged by
+// 16-B LDS-DMA instead of dword loads into registers. Round-5 PMC of k1n on 20x96x54^2 -> 96
+// (profiles/r05/pmc_k1n.json): 59.5 % of wave cycles in s_waitcnt on the input stream. Its in-flight
+// input is capped by the vmcnt counter, which the loads share with the epilogue's 16 TM stores:
+// (Q - 1) KC / 2 + 16 TM <= 63, so the 96-channel tile that reads each input pixel once could keep only
+// ~3 KB per wave in flight (kn96*: slower than kn32, which re-reads the input per 32-channel tile). Here
+// one 16-B DMA instruction moves 1 KB (eight channel rows of a unit's 32 pixels) where a dword load
+// moved 256 B, so the same counter holds 4x the bytes, and the in-flight data needs no registers:
+//  * the block holds the WHOLE bank [K][OCP] (OC rounded up to the unit's channels) and the biases in
+//    LDS (IC * OC small enough), loaded once; a unit is 32 consecutive pixels of the flattened (image,
+//    pixel) space x one sub-tile of OCT = 32 TM channels x all K; units are dealt to the grid's waves
+//    round-robin (sub-tile fastest: a pixel group's sub-tiles run on neighbouring waves of one block,
+//    so the re-read input comes from L1 / L2);
+//  * each wave streams its units' input through its own ring of D slots [KC][32] (no barrier after the
+//    prologue: a wave's DMA and its ds_reads of a slot are ordered by its own vmcnt wait), D - 1 chunks
+//    ahead, across unit boundaries;
+//  * step s of a chunk: A = bank row 2 s + kh (one ds_read_b32 per 32-channel tile), B = slot row
+//    2 s + kh, column li (one ds_read_b32), TM MFMAs; biases as the first MFMA's C, epilogue as k1n
+//    (TN = 1: one dword store per output row and lane, rows' offsets scalar).
+// vmcnt: waiting for chunk g, the younger VMEM ops are the DMAs of chunks g+1 .. g+D-2 ((D-2) L) plus,
+// when an epilogue ran after chunk g's DMA was issued (chunk index in its unit < D - 1), its S stores;
+// S dropped stores after the prologue give the first unit the same sequence (as k1n). K / KC >= D - 1.
+// DBG (instrumented library only, wrong results by design): bit 0 = the epilogue's stores dropped (OOB)
+template <int TM, int KC, int D, int NW, int DBG = 0>
+__global__ __launch_bounds__(NW * 64) void k1d_kernel(GemmArgs p) {
+  constexpr int OCT = 32 * TM;
+  constexpr int SC = KC / 2;   // k steps per chunk
+  constexpr int L = KC / 8;    // 16-B DMA instructions per chunk and wave
+  constexpr int S = 16 * TM;   // dword stores per lane per unit
+  constexpr int PF = 3;        // LDS fragment prefetch (steps)
+  constexpr int CH = KC * 32;  // floats per ring slot
+  static_assert(TM >= 1 && TM <= 3 && KC % 8 == 0 && SC % (PF + 1) == 0, "tile");
+  static_assert(D >= 3 && (D - 2) * L + S <= 63, "vmcnt range");
+  // [K][OCP] bank, [OCP rounded up to 64] biases, then each wave's ring [D][KC][32]
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  KT(0);
+  const uint32_t OCP = p.tbm, ntm = p.tiles_m, nch = p.K / KC;
+  const uint32_t U = p.total_it;  // units: pixel groups x OC sub-tiles
+  const uint32_t W = gridDim.x * NW, w0 = blockIdx.x * NW + (uint32_t)wave;
+  const uint32_t hw4 = p.HW * 4u, ohw4 = p.OHW * 4u;
+  const uint32_t BREG = (OCP + 63) / 64 * 64;  // bias region: whole 64-lane DMAs
+  float *const bl = wl + p.K * OCP;
+  float *const ring = bl + BREG + wave * (D * CH);
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsx = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+
+  // ---- resident bank and biases: piece e = (row k, columns 4q ..) of [K][OCP]; columns past OC4 miss
+  {
+    const uint32_t pr = OCP / 4, np = p.K * pr;
+    // (np is a multiple of 64: a wave's DMA lies wholly inside the bank or is not issued -- a DMA past
+    // the end would write over the biases and rings; no wait counts on these, they are older than all)
+    for (uint32_t e0 = (uint32_t)wave * 64; e0 < np; e0 += NW * 64) {
+      const uint32_t e = e0 + (uint32_t)lane, k = e / pr, q = e - k * pr;
+      dma16(rsw, wl + 4 * e0, oob_unless(4 * q < p.lda, (k * p.lda + 4 * q) * 4u));
+    }
+    for (uint32_t c0 = (uint32_t)wave * 64; c0 < OCP; c0 += NW * 64) {
+      const uint32_t c = c0 + (uint32_t)lane;
+      dma4(rsbias, bl + c0, oob_unless(c < p.M, c * 4u));
+    }
+  }
+  // ---- the wave's units u = w0 + i W; lane e of a chunk DMA: channel row e / 8 (+ 8 j), pixels 4 (e % 8)
+  auto unit_of = [&](uint32_t u, uint32_t &pu, uint32_t &ocs) {
+    pu = fdiv(u, p.tm_m, p.tm_s);
+    ocs = u - pu * ntm;
+  };
+  auto dbase = [&](uint32_t u) -> uint32_t {  // this lane's DMA source offset of unit u (channel 0)
+    uint32_t pu, ocs;
+    unit_of(u, pu, ocs);
+    const uint32_t n = pu * 32u + 4u * (uint32_t)(lane & 7);
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    return oob_unless((u < U) & (n < p.N), (img * p.ICHW + pix + (uint32_t)(lane >> 3) * p.HW) * 4u);
+  };
+  uint32_t u = w0;
+  uint32_t bcur = dbase(u), bnext = dbase(u + W);
+  auto issue = [&](uint32_t slot, uint32_t base, uint32_t c) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) dma16s(rsx, ring + slot * CH + j * 256, base, (c * KC + 8 * j) * hw4);
+  };
+  // prologue: chunks 0 .. D-2 of the first unit (K / KC >= D - 1), then S dropped stores
+#pragma unroll
+  for (int q = 0; q < D - 1; ++q) issue((uint32_t)q, bcur, (uint32_t)q);
+#pragma unroll
+  for (int s = 0; s < S; ++s) __builtin_amdgcn_raw_buffer_store_b32(0u, rso, OOB, 0, 0);
+  vm_wait<(D - 2) * L + S>();  // the bank, the biases and chunk 0 landed (this wave's DMAs) ...
+  __syncthreads();             // ... every wave's
+  if (u >= U) return;
+
+  f32x16 acc[TM];
+  float wf[PF + 1][TM], xf[PF + 1];
+  uint32_t pu, ocs;
+  unit_of(u, pu, ocs);
+  const float *wa = wl + kh * OCP + ocs * OCT + li;  // bank fragment base of the unit's sub-tile
+  const float *const xa = ring + kh * 32 + li;       // slot fragment base (+ slot * CH)
+  auto frag = [&](int b, uint32_t slot, uint32_t c, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) wf[b][t] = wa[(c * KC + 2 * s) * OCP + 32 * t];
+    xf[b] = xa[slot * CH + 2 * s * 32];
+  };
+  auto load_bias = [&]() {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4v b4 = *(const f32x4v *)(bl + ocs * OCT + 32 * t + 8 * g + 4 * kh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[t][4 * g + e] = b4[e];
+      }
+  };
+  const float floor0 = p.relu ? 0.0f : __builtin_nanf("");  // relu_floor: NaN = no clamp
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  auto epilogue = [&](auto masked, auto res, auto wt) {
+    uint32_t h4 = ohw4;
+    asm volatile("" : "+s"(h4));
+    const uint32_t oc0 = ocs * OCT, so0 = oc0 * h4;
+    const uint32_t n = pu * 32u + (uint32_t)li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    const uint32_t ob = (DBG & 1) ? OOB : oob_unless(n < p.N, (img * p.OCOHW + pix) * 4u + (uint32_t)(4 * kh) * h4);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t so = so0 + (uint32_t)(32 * t + 8 * g + i) * h4;
+          uint32_t o = ob;
+          if constexpr (decltype(masked)::value) o = oob_unless(oc0 + (uint32_t)(32 * t + 8 * g + 4 * kh + i) < p.M, ob);
+          float v = acc[t][4 * g + i];
+          if constexpr (decltype(res)::value) v += ldv<1>(rsr, o, so);
+          v = relu_floor(v, floor0);
+          if constexpr (decltype(wt)::value) stv<1, AUX_SC1>(v, rso, o, so);
+          else stv<1, AUX_OUT>(v, rso, o, so);
+        }
+  };
+  auto epilogue_m = [&](auto masked) {
+    if (p.res) {
+      if (p.wt) epilogue(masked, std::true_type{}, std::true_type{});
+      else epilogue(masked, std::true_type{}, std::false_type{});
+    } else {
+      if (p.wt) epilogue(masked, std::false_type{}, std::true_type{});
+      else epilogue(masked, std::false_type{}, std::false_type{});
+    }
+  };
+
+  // the chunk stream: chunk c of the current unit sits in slot `slot`; the DMA issued with it is chunk
+  // c + D - 1 (of this unit, or the next one's chunk c + D - 1 - nch) into the slot freed last chunk.
+  // The first PF steps' fragments of the NEXT chunk are read in the last PF steps of this one, after
+  // that chunk's wait: younger than its DMA are the DMAs of the D - 2 chunks after it, and, when its
+  // index in its unit is 1 .. D - 2, the S stores of the epilogue that ran since it was issued
+  uint32_t slot = 0, islot = D - 1;
+  load_bias();
+#pragma unroll
+  for (int s = 0; s < PF; ++s) frag(s, 0, 0, s);  // chunk 0 landed (prologue wait)
+  for (;;) {
+    // the next unit's sub-tile: the last chunk prefetches its first fragments
+    uint32_t pu_n, ocs_n;
+    unit_of(u + W, pu_n, ocs_n);
+    const float *const wa_n = wl + kh * OCP + ocs_n * OCT + li;
+    for (uint32_t c = 0; c < nch; ++c) {
+      {
+        const uint32_t c2 = c + (uint32_t)(D - 1);
+        const bool nx = c2 >= nch;
+        issue(islot, nx ? bnext : bcur, nx ? c2 - nch : c2);
+      }
+      const uint32_t nslot = slot == D - 1 ? 0u : slot + 1;
+      const bool last = c + 1 == nch;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < SC; ++s) {
+        if (s + PF < SC) {
+          frag((s + PF) % (PF + 1), slot, c, s + PF);
+        } else {
+          if (s + PF == SC) {  // the next chunk's DMA (uniform)
+            if (!last && c + 1 <= (uint32_t)(D - 2)) vm_wait<(D - 2) * L + S>();
+            else vm_wait<(D - 2) * L>();
+          }
+          if (last) {
+            const float *const wsave = wa;
+            wa = wa_n;
+            frag((s + PF) % (PF + 1), nslot, 0, s + PF - SC);
+            wa = wsave;
+          } else {
+            frag((s + PF) % (PF + 1), nslot, c + 1, s + PF - SC);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s % (PF + 1)][t], xf[s % (PF + 1)], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      islot = slot;
+      slot = nslot;
+    }
+    // every unit issues exactly S stores (dropped where masked or past the op): the waits count them
+    if (ocs * OCT + OCT <= p.M) epilogue_m(std::false_type{});
+    else epilogue_m(std::true_type{});
+    u += W;
+    if (u >= U) break;
+    bcur = bnext;
+    bnext = dbase(u + W);
+    pu = pu_n;
+    ocs = ocs_n;
+    wa = wa_n;
+    load_bias();
+  }
+  vm_wait<0>();
+}
+
+template <int TM, int KC, int D, int NW, int DBG = 0>
+cfg_t k1d_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * NW, KC, 64 * NW, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = k1d_kernel<TM, KC, D, NW, DBG>;
+  c.dc = 3;
+  c.dc_ky = 1;
+  c.dc_kx = 1;
+  c.dc_ci = KC;
+  c.dc_rin = D;
+  c.k1d = 1;
+  return c;
+}
+
 template <int TM, int TN, int KC, int Q, int NW>
 cfg_t k1n_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * TN * NW, KC, 64 * NW, {}, 1};
@@ -553,11 +778,65 @@ std::vector<cfg_t> k1s_cfgs() {
       k1n_cfg<2, 2, 16, 4, 4>("kn64p64c16q4w4"),   k1n_cfg<3, 1, 8, 4, 8>("kn96p32c8q4w8"),
       k1n_cfg<3, 2, 8, 4, 8>("kn96p64c8q4w8"),     k1n_cfg<3, 2, 16, 2, 8>("kn96p64c16q2w8"),
       k1n_cfg<3, 2, 8, 4, 4>("kn96p64c8q4w4"),
+      // k1d <TM, KC, D, NW>: kd<OC sub-tile>c<KC>d<ring slots>w<NW>, the whole bank resident
+      k1d_cfg<3, 16, 6, 4>("kd96c16d6w4"), k1d_cfg<3, 16, 8, 4>("kd96c16d8w4"), k1d_cfg<3, 16, 5, 8>("kd96c16d5w8"),
+      k1d_cfg<2, 16, 6, 4>("kd64c16d6w4"), k1d_cfg<2, 16, 8, 4>("kd64c16d8w4"), k1d_cfg<2, 16, 5, 8>("kd64c16d5w8"),
+      k1d_cfg<2, 32, 4, 4>("kd64c32d4w4"), k1d_cfg<1, 32, 5, 4>("kd32c32d5w4"), k1d_cfg<1, 16, 5, 8>("kd32c16d5w8"),
+      k1d_cfg<3, 32, 3, 4>("kd96c32d3w4"),
+      // D = K / KC + 1: a unit's whole input is in flight before the previous unit's stores go out, so no
+      // ring wait orders behind a store (vmcnt counts loads, DMAs and stores in issue order)
+      k1d_cfg<3, 32, 4, 4>("kd96c32d4w4"), k1d_cfg<3, 16, 7, 4>("kd96c16d7w4"), k1d_cfg<2, 32, 3, 4>("kd64c32d3w4"),
+      k1d_cfg<2, 16, 5, 4>("kd64c16d5w4"), k1d_cfg<2, 32, 3, 8>("kd64c32d3w8"), k1d_cfg<1, 32, 4, 4>("kd32c32d4w4"),
+      k1d_cfg<1, 32, 3, 8>("kd32c32d3w8"),
+#ifdef BH_KTRACE
+      k1d_cfg<3, 32, 4, 4, 1>("xkd96c32d4w4_nostore"), k1d_cfg<3, 16, 6, 4, 1>("xkd96c16d6w4_nostore"),
+#endif
 #ifdef BH_KTRACE
       k1s_cfg<3, 32, 3, 4, 1>("xks96c32q3_noload"), k1s_cfg<3, 32, 3, 4, 2>("xks96c32q3_nomfma"),
       k1s_cfg<3, 32, 3, 4, 4>("xks96c32q3_nostore"), k1s_cfg<3, 32, 3, 4, 7>("xks96c32q3_none"),
 #endif
   };
+}
+
+// k1d: the whole bank [K][OCP] + biases + NW rings of D chunks [KC][32] in LDS; K a whole number of
+// chunks, at least D - 1 of them; OH*OW % 4 == 0 and a 16-B aligned input (16-B DMA pieces of 4 pixels
+// never straddle two images). splits: 0 = as many blocks per CU as fit (at most 4), 1..4 = blocks per
+// CU, 8 = one unit per wave (the whole grid queued)
+int launch_k1d(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t splits, bool first) {
+  const uint32_t KC = (uint32_t)c.dc_ci, D = (uint32_t)c.dc_rin, NW = (uint32_t)c.NT / 64, BM = (uint32_t)c.BM;
+  if (p.K % KC || p.K / KC < D - 1)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs input channels a multiple of " +
+                                  std::to_string(KC) + ", at least " + std::to_string((D - 1) * KC));
+  if (p.OHW % 4 || (uintptr_t)p.b % 16)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs OH*OW % 4 == 0 and a 16-B aligned input");
+  const uint32_t ocp = (p.M + BM - 1) / BM * BM, ntm = ocp / BM;
+  const uint64_t lds = ((uint64_t)p.K * ocp + (ocp + 63) / 64 * 64 + (uint64_t)NW * D * KC * 32) * 4;
+  if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: bank too large for ") + c.name);
+  const uint64_t out_bytes = (uint64_t)p.OCOHW * (p.N / p.OHW) * 4;
+  if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the k1d kernel");
+  p.c_bytes = (uint32_t)out_bytes;
+  const uint64_t units = (uint64_t)((p.N + 31) / 32) * ntm;
+  if (units >= (1u << 31)) return bh::fail(BH_UNSUP, "conv: k1d grid too large");
+  const void *k = (const void *)c.k[A_KVEC][B_DIRECT][0];
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return bh::fail(BH_ERR, "conv: k1d LDS attribute");
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, c.NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
+  const uint32_t ncu = ctx->prop.multiProcessorCount > 0 ? ctx->prop.multiProcessorCount : 256;
+  const uint64_t need = (units + NW - 1) / NW;  // blocks for one unit per wave
+  uint64_t G = need;
+  if (splits < 8) G = std::min<uint64_t>(need, (uint64_t)ncu * std::min<uint32_t>(splits ? splits : 4, (uint32_t)std::min(occ, 4)));
+  p.tbm = ocp;
+  p.tiles_m = ntm;
+  p.total_it = (uint32_t)units;
+  bh::fastdiv f = bh::make_fastdiv(ntm);
+  p.tm_m = f.m;
+  p.tm_s = f.s;
+#ifdef BH_KTRACE
+  p.trace = (unsigned long long *)ctx->stamps + 65536;
+#endif
+  void *args[] = {&p};
+  return bh::launch(ctx, k, dim3((uint32_t)G, 1, 1), dim3(c.NT), args, first, true, "conv_k1d", (uint32_t)lds);
 }
 
 // Launch a resident-bank 1x1 configuration (p filled by launch_conv with a = packed bank): UNSUP
@@ -571,6 +850,7 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   if (KY != 1 || KX != 1 || sy != 1 || sx != 1 || p.py || p.px)
     return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " is for unpadded stride-1 1x1 convs");
   const uint32_t KC = (uint32_t)c.dc_ci, Q = (uint32_t)c.dc_rin, NT = (uint32_t)c.NT;
+  if (c.k1d) return launch_k1d(ctx, c, p, splits, first);
   if (p.K % KC || (p.K / KC) % Q)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a whole number of ") + c.name + " trips");
   // k1n: a lane's gv_cx pixels lie in one image (OH*OW % gv_cx == 0) and its vector loads / stores

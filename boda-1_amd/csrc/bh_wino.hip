@@ -109,6 +109,13 @@ __device__ __forceinline__ uint32_t wg_lb(uint32_t bid, uint32_t G) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// x where the lane's bit of m is set, else 0 (one v_cndmask against a wave mask held in SGPRs)
+__device__ __forceinline__ float wg_lane_sel(uint64_t m, float x) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
+  return r;
+}
+
 __device__ __forceinline__ void wg_store1(const WgArgs &p, __amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
   if (p.wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_SC1);
   else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX_OUT);
@@ -251,6 +258,19 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   // (half h = tid / (4 TT): wave-uniform, so the two halves' different arithmetic does not diverge)
   const uint32_t xpr = (uint32_t)tid % (WCI * TT), xh = __builtin_amdgcn_readfirstlane((uint32_t)tid / (WCI * TT));
   const uint32_t xcl = xpr / TT, xtt = xpr % TT;
+  // IL == 2 (configs wgl*): the TS == 2 transform with no per-half selects and fewer masks, per-lane
+  // LDS bases made once per tile, the strip slot and V buffer of a stage one phase counter. Half h = 0 reads patch rows 0, 1, 2, half 1 rows 2, 3, 1 (into e0, e1, e2):
+  // V rows 2h, 2h + 1 come from t0 = e0 - e2 (h0: r0 - r2, h1: r2 - r1) and t1 = e2 + sg e1 (sg = +1:
+  // r1 + r2, sg = -1: r1 - r3) -- the same roundings as the per-half forms (bitwise equal V). Only patch
+  // columns 2 and 3 ever reach past the row (x = 2 tx - px, pad <= 1) and column 0 before it (x = -1
+  // reads the previous strip row's last column: a 16-B piece's spill from the next input row when
+  // W % 4 != 0); column 1 never leaves it. Masking a column of t masks that column of the patch (each t
+  // column combines one patch column): 6 selects instead of 12.
+  constexpr bool LEAN = IL == 2;
+  static_assert(!LEAN || (TS == 2 && D == 3), "lean transform: two threads per patch, three strip slots");
+  const float *xp[3] = {smem, smem, smem};
+  uint64_t cm0 = ~0ull, cm2 = ~0ull, cm3 = ~0ull;
+  const float sg = xh ? -1.0f : 1.0f;
   uint32_t xb = GZ;
   uint32_t xm = 0xfu;  // !V4: patch columns inside the row (the rest of a 16-B piece is the next row's)
   uint32_t lx_tile = 0xffffffffu;
@@ -272,6 +292,15 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
       xm = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) xm |= ((uint32_t)(x + c) < p.W ? 1u : 0u) << c;
+    }
+    if constexpr (LEAN) {  // the half's three patch rows (xh = 1 reads them permuted), column masks
+#pragma unroll
+      for (int r = 0; r < 3; ++r) xp[r] = smem + xb + (xh ? (r == 0 ? 2u : (r == 1 ? 3u : 1u)) : (uint32_t)r) * p.WPM;
+      if constexpr (!V4) {
+        cm0 = __builtin_amdgcn_ballot_w64((xm & 1u) != 0);
+        cm2 = __builtin_amdgcn_ballot_w64(((xm >> 2) & 1u) != 0);
+        cm3 = __builtin_amdgcn_ballot_w64(((xm >> 3) & 1u) != 0);
+      }
     }
   };
   // TS == 1: patch rows 0..3, all four V rows; TS == 2: half h reads rows h .. h + 2 (d[0..2]) and
@@ -381,6 +410,40 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
       } else if (part == 5) {
         put(2 * xh + 1, tq[1]);
       }
+    }
+  };
+
+  float *const vput0 = vbase + (xcl * TT + xtt) * 16 + ((2u * xh + ((xtt >> 2) & 3u)) & 3u) * 4;
+  float *const vput1 = vbase + (xcl * TT + xtt) * 16 + ((2u * xh + 1u + ((xtt >> 2) & 3u)) & 3u) * 4;
+  auto tx_read_l = [&](int sl) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[r][c] = xp[r][sl * SLOT + c];
+  };
+  auto tx_part_l = [&](int vb_, int part) {
+    auto put = [&](float *vd, const float (&t)[4]) {
+      *(f32x4v *)(vd + vb_ * VSZ) = f32x4v{t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+    };
+    if (part == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) tq[0][c] = d[0][c] - d[2][c];
+    } else if (part == 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) tq[1][c] = __builtin_fmaf(sg, d[1][c], d[2][c]);
+    } else if (part == 2) {
+      if constexpr (!V4) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          tq[r][0] = wg_lane_sel(cm0, tq[r][0]);
+          tq[r][2] = wg_lane_sel(cm2, tq[r][2]);
+          tq[r][3] = wg_lane_sel(cm3, tq[r][3]);
+        }
+      }
+    } else if (part == 3) {
+      put(vput0, tq[0]);
+    } else if (part == 4) {
+      put(vput1, tq[1]);
     }
   };
 
@@ -552,12 +615,21 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  xplan(it0);
-  tx_read(0);
-  tx_write(0);
-  xplan(it0 + 1);
-  tx_read(1);
-  tx_write(1);
+  if constexpr (LEAN) {
+    xplan(it0);
+    tx_read_l(0);
+    for (int q = 0; q < 5; ++q) tx_part_l(0, q);
+    xplan(it0 + 1);
+    tx_read_l(1);
+    for (int q = 0; q < 5; ++q) tx_part_l(1, q);
+  } else {
+    xplan(it0);
+    tx_read(0);
+    tx_write(0);
+    xplan(it0 + 1);
+    tx_read(1);
+    tx_write(1);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -663,6 +735,65 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     sl2 = sl2 == D - 1 ? 0 : sl2 + 1;
   };
 
+  // IL == 2: stage it at phase ph = (it - it0) % 3 -- V(it) in buffer ph, V(it+1) in ph + 1, stage it+2's
+  // strip in slot ph + 2 (transformed into V buffer ph + 2), stage it+D+1's strip issued into slot ph + 1
+  // (D == 3: the slot and buffer rotations coincide; a phase-unrolled form, every LDS address an
+  // immediate, took 256 VGPRs and spilled)
+  const float *vfq[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) vfq[x] = vbase + ((uint32_t)kh * TT + (uint32_t)(wtl * 32 + li)) * 16 + co[x];
+  auto stage_l = [&](uint32_t it, uint32_t ph) {
+    const int vb1 = ph == 2 ? 0 : (int)ph + 1, vb2 = ph == 0 ? 2 : (int)ph - 1;
+    vm_wait<WTOP>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    xplan(it + 2);
+    tx_read_l(vb2);
+    uint32_t ss = 0;
+    const bool dead = plan_strip(it + D + 1, ss);
+    const uint32_t su = plan_u(it + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int QG = (SP + 3) / 4;
+    auto mf = [&](int st, int x, int n) {
+      acc[4 * x + n] = __builtin_amdgcn_mfma_f32_32x32x2f32(ur[st][x][n], vf[st][x][n], acc[4 * x + n], 0, 0, 0);
+    };
+    auto chunk = [&](int st, int x) {  // stage it+1's U and V fragments of chunk x, k step st
+      ur[st][x] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rsu, uoff[st][x], su, 0));
+      vf[st][x] = *(const f32x4v *)(vfq[x] + vb1 * VSZ + 2 * st * TT * 16);
+    };
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int st = x >> 1, c0 = 2 * (x & 1), c1 = c0 + 1;
+      vm_wait<6 + SP>();  // U(it) group x landed
+      mf(st, c0, 0);
+      mf(st, c0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      tx_part_l(vb2, 2 * x);
+      __builtin_amdgcn_sched_barrier(0);
+      mf(st, c0, 2);
+      mf(st, c0, 3);
+      __builtin_amdgcn_sched_barrier(0);
+      chunk(st, c0);
+      __builtin_amdgcn_sched_barrier(0);
+      mf(st, c1, 0);
+      mf(st, c1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      tx_part_l(vb2, 2 * x + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mf(st, c1, 2);
+      mf(st, c1, 3);
+      __builtin_amdgcn_sched_barrier(0);
+      chunk(st, c1);
+#pragma unroll
+      for (int j = x * QG; j < (x + 1) * QG; ++j) {
+        if (j < SP) issue_strip(j, vb1, ss, dead);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  uint32_t ph = 0;  // (it - it0) % 3, IL == 2
+
   uint32_t it = it0;
   while (it < it1) {
     const uint32_t t = fdiv(it, p.ipt_m, p.ipt_s);
@@ -680,7 +811,14 @@ __global__ __launch_bounds__(64 * NWO * NWT) void wgp_kernel(WgArgs p) {
     for (int q = 0; q < 16; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
-    for (; it < iend; ++it) stage(it);
+    if constexpr (LEAN) {
+      for (; it < iend; ++it) {
+        stage_l(it, ph);
+        ph = ph == 2 ? 0u : ph + 1;
+      }
+    } else {
+      for (; it < iend; ++it) stage(it);
+    }
 #ifdef BH_KTRACE
     tkp = __builtin_amdgcn_s_memtime();
 #endif
@@ -831,6 +969,8 @@ std::vector<cfg_t> wg_cfgs() {
       wgp_cfg<2, 2, 3, 1, 4, 1>("wgi64x64v"), wgp_cfg<2, 2, 3, 0, 3, 1>("wgi64x64"),
       wgp_cfg<2, 2, 4, 1, 3, 1>("wgi64x64vd4"), wgp_cfg<2, 2, 4, 0, 3, 1>("wgi64x64d4"),
       wgp_cfg<4, 1, 3, 1, 2, 1>("wgi128x32v"), wgp_cfg<4, 1, 3, 0, 2, 1>("wgi128x32"),
+      // lean transform, stage loop unrolled over the buffers (round 6)
+      wgp_cfg<4, 1, 3, 1, 2, 2>("wgl128x32v"), wgp_cfg<4, 1, 3, 0, 2, 2>("wgl128x32"),
 #ifdef BH_WG_DIAG
       // diagnostic builds (wrong results by design): one part of the stage dropped each
       wgp_cfg<4, 1, 3, 0, 2, 0, 1>("xwgp_noxf"), wgp_cfg<4, 1, 3, 0, 2, 0, 2>("xwgp_nomfma"),

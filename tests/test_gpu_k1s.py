@@ -22,24 +22,38 @@ from test_gpu_conv import run_conv
 
 pytestmark = pytest.mark.gpu
 
-KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("ks", "kn"))]
+KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("ks", "kn", "kd"))]
 
 
 def trip_of(name):
+    if name.startswith("kd"):  # kd<OCT>c<KC>d<D>w<NW>: K a multiple of KC (and >= (D - 1) KC: min_k)
+        return int(re.match(r"kd\d+c(\d+)", name).group(1))
     kc, q = map(int, re.match(r"k[sn]\d+(?:p\d+)?c(\d+)q(\d+)", name).groups())
     return kc * q
 
 
+def min_k(name):
+    m = re.match(r"kd\d+c(\d+)d(\d+)", name)
+    return int(m.group(1)) * (int(m.group(2)) - 1) if m else 0
+
+
 def tn_of(name):
     """Pixels per lane of a kn configuration (1 for ks)."""
+    if name.startswith("kd"):  # 16-B input pieces of 4 pixels never straddle two images
+        return 4
     m = re.match(r"kn\d+p(\d+)", name)
     return int(m.group(1)) // 32 if m else 1
 
 
-def fits(name, ic):
+def fits(name, ic, oc=None, ohw=None):
     """ks: the bank slice [IC][OCT] and the waves' [32][36] epilogue tiles fit the LDS; kn: the
-    bank slice and the tile's biases (whole 64-float DMAs)."""
-    oct_ = int(re.match(r"k[sn](\d+)", name).group(1))
+    bank slice and the tile's biases (whole 64-float DMAs); kd: the whole bank [IC][OC rounded to
+    the sub-tile], the biases and every wave's ring [D][KC][32], with OH*OW % 4 == 0."""
+    oct_ = int(re.match(r"k[sdn](\d+)", name).group(1))
+    if name.startswith("kd"):
+        kc, d, nw = map(int, re.match(r"kd\d+c(\d+)d(\d+)w(\d+)", name).groups())
+        ocp = -(-oc // oct_) * oct_
+        return (ic * ocp + -(-ocp // 64) * 64 + nw * d * kc * 32) * 4 <= 160 * 1024 and ohw % 4 == 0 and ic >= min_k(name)
     if name.startswith("kn"):
         return (ic * oct_ + -(-oct_ // 64) * 64) * 4 <= 160 * 1024
     nw = 8 if name.endswith("w8") else 4
@@ -50,7 +64,8 @@ def k1(b, ic, h, w, oc):
     return ops.ConvShape(b, ic, h, w, oc, 1, 1, 1, 1, 0, 0)
 
 
-SHAPES = [k1(2, 96, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(1, 96, 28, 28, 130), k1(5, 192, 6, 6, 64),
+SHAPES = [k1(2, 96, 54, 54, 96), k1(1, 64, 56, 56, 64), k1(2, 192, 28, 28, 96),  # the conv set's big-pixel shapes
+          k1(2, 96, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(1, 96, 28, 28, 130), k1(5, 192, 6, 6, 64),
           k1(2, 96, 7, 9, 40), k1(2, 64, 14, 14, 64), k1(1, 128, 27, 27, 256), k1(3, 256, 7, 7, 48),
           k1(1, 288, 5, 5, 33), k1(1, 64, 1, 1, 20), k1(4, 384, 13, 13, 100),
           k1(2, 192, 12, 12, 72), k1(3, 128, 10, 10, 100)]  # OH*OW % 4 == 0, ragged OC: kn's masked rows
@@ -71,7 +86,7 @@ def test_ks_config(dev, cn):
         for s in SHAPES:
             if s.IC % trip_of(cn):
                 continue
-            if not fits(cn, s.IC) or (s.OH * s.OW) % tn_of(cn):
+            if not fits(cn, s.IC, s.OC, s.OH * s.OW) or (s.OH * s.OW) % tn_of(cn):
                 dev.tune_set(1, ci, 0)
                 with pytest.raises(boda_hip.UnsupportedError):
                     run_conv(dev, s)
@@ -100,6 +115,9 @@ def test_ks_rejects(dev, cn):
                   k1(1, t + 16, 13, 13, 16)):                          # K not a whole number of trips
             with pytest.raises(boda_hip.UnsupportedError):
                 run_conv(dev, s)
+        if min_k(cn) > t:  # fewer input channels than the ring's prologue holds
+            with pytest.raises(boda_hip.UnsupportedError):
+                run_conv(dev, k1(1, t, 12, 12, 16))
         if tn_of(cn) > 1:  # a lane's pixels would straddle two images
             with pytest.raises(boda_hip.UnsupportedError):
                 run_conv(dev, k1(2, t, 7, 7, 16))
@@ -108,7 +126,7 @@ def test_ks_rejects(dev, cn):
 
 
 @pytest.mark.parametrize("cn,s", [(cn, s) for cn in ("ks96c32q3", "ks64c16q4", "kn96p32c8q4w8", "kn64p64c16q3w8",
-                                                    "kn32p128c16q4w4")
+                                                    "kn32p128c16q4w4", "kd96c16d6w4", "kd64c16d6w4", "kd32c32d5w4")
                                   for s in (k1(2, 192, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(2, 192, 12, 12, 72))
                                   if (s.OH * s.OW) % tn_of(cn) == 0])
 def test_ks_residual_and_slab(dev, cn, s):

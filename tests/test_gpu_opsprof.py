@@ -86,7 +86,7 @@ def test_ops_prof_all_is_well(suite, ops_fn, mode, nops, tmp_path):
 # cross-implementation compare to 4e-4 (cuDNN, test_cmds.xml:110) for kernels that sum in the same
 # order; an element-wise 2e-4 across summation orders is not attainable in fp32.
 TUNES = ("(kg=(use_be=hip,cfg=ref64),tab=(use_be=hip),dm=(cfg=dm3w16x64c8),tile=(cfg=128x128x32),gvs=(cfg=gvs64x32w8),"
-         "wx43=(cfg=wx43s12),wx23=(cfg=wx23s6),wx25=(cfg=wx25s6),wgi=(cfg=wgi128x32))")
+         "wx43=(cfg=wx43s12),wx23=(cfg=wx23s6),wx25=(cfg=wx25s6),wgi=(cfg=wgi128x32),wgl=(cfg=wgl128x32))")
 MULTI = [("conv-debug", None), ("ops-prof-conv-3x3-cudnn-boda", 37)]
 
 
@@ -115,11 +115,13 @@ def test_ops_prof_multi_tune_vs_kg(suite, outlier, tmp_path, golden):
     else:  # the reference's own stored digest of this op is off by 1.22x its tolerance
         assert all(int(x[0]) == outlier and "_wino_" not in x[2] for x in bad), bad
         worst = [float(x) for x in re.findall(r"worst rd/tol ([\d.]+)", r.stdout)]
-        # the exact (kg) sum misses that stored digest by 1.22x; a direct fp32 route whose own element
-        # error reaches 1.2e-3 (dm3 at K = 3456, profiles/r05/route_acc_3x3.txt) lands up to ~1.7x
-        # from it (round 5) -- every route is checked against the exact sum by the live compare above
+        # the exact (kg) sum misses that stored digest by 1.22x; the direct fp32 routes land 1.27-1.74x
+        # from it, per tune (profiles/r06/opsprof_op37_multitune.log: kg 1.219, tab 1.268, dm3
+        # 1.278, the split-K tile kernel 1.736; gvs and the Winograd tunes at their 2e-3 pass) -- the
+        # kernels are deterministic, so these are the values every run sees; every route is checked
+        # against the exact sum by the live compare above
         kg_bad = [x for x in bad if x[1] == "kg"]
-        assert not worst or max(worst) < 2.0, (worst, ["%s:%s" % (x[1], x[2]) for x in bad])
+        assert not worst or max(worst) < 1.8, (worst, ["%s:%s" % (x[1], x[2]) for x in bad])
         assert len(kg_bad) <= 1 and min(worst, default=0) < 1.5, (worst, kg_bad)
     st = subprocess.run([os.path.join(BIN, "boda_hip_ops_prof"), "--selftest-wisdom=" + str(tmp_path / "out.wis")],
                         capture_output=True, text=True, timeout=60)

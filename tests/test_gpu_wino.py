@@ -72,6 +72,10 @@ def test_wg_config(dev, cn):
                 outs[splits] = out
                 if splits >= 20:  # the separate combine kernel sums the same slabs in the same order
                     np.testing.assert_array_equal(out, outs[splits - 20])
+                if cn.startswith("wgl"):  # the lean transform makes the same V: bitwise the wgi route
+                    dev.tune_set(1, boda_hip.tune_cfg_names(1).index("wgi" + cn[3:]), splits)
+                    np.testing.assert_array_equal(run_conv(dev, s), out)
+                    dev.tune_set(1, ci, splits)
     finally:
         dev.tune_set(1, -1, 0)
     assert ran >= 8, "config %s ran on too few shapes" % cn
