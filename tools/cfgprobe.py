@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--sgemm", action="append", default=[])
     ap.add_argument("--top", type=int, default=0, help="take the N conv ops with the largest loss in --perop")
     ap.add_argument("--perop", default=os.path.join(ROOT, "profiles", "r01", "bench_perop.json"))
-    ap.add_argument("--cfg", default="r", help="config-name prefix filter")
+    ap.add_argument("--cfg", action="append", default=[], help="config-name prefix filter (repeatable; default r)")
     ap.add_argument("--splits", default="1")
     ap.add_argument("--json", default="")
     ap.add_argument("--no-table", action="store_true", help="compare against the untuned heuristic")
@@ -53,7 +53,7 @@ def main():
         rf = runner.roofline_secs(s) * 1e3
         print("%s  tuned %.4f ms (%.0f%% roofline)" % (s, t0, 100 * rf / t0), flush=True)
         for ci, cn in enumerate(boda_hip.tune_cfg_names(kind)):
-            if not cn.startswith(a.cfg):
+            if not cn.startswith(tuple(a.cfg or ["r"])):
                 continue
             for S in map(int, a.splits.split(",")):
                 dev.tune_set(kind, ci, S)
