@@ -453,7 +453,8 @@ __global__ __launch_bounds__(256) void dc_kernel(GemmArgs p) {
 // DBG (diagnostic builds in the instrumented library only; wrong results by design): bit 0 = no strip DMA
 // after the prologue, 1 = no MFMA, 2 = no output stores, 3 = no stage barrier, 4 = no B (strip) fragment
 // reads, 5 = no A (weight) fragment reads
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0,
+          int PSL = 0>
 __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   constexpr int NT = NW * 64, NPX = NW * 32, OCT = 32 * TM;
   constexpr int KK = KY * KX, KK2 = (KK + 1) / 2;
@@ -464,6 +465,8 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
   constexpr int SF = RIN * WPM;
   constexpr int PW = V4 ? 4 : 1;
   static_assert(WPM % PW == 0, "16-B strip rows");
+  static_assert(!PSL || (!V4 && WPM % S == 0), "phase-split strip: dword DMA, whole phases per row");
+  constexpr int WS = WPM / S;                               // PSL: strip floats per column phase
   constexpr int LWB = (SF / PW + NT - 1) / NT;              // strip DMA instructions per wave and stage
   constexpr int SREG = LWB * NT * PW;                       // floats per strip slot
   static_assert(D >= 2 && (D - 2) * LWB <= 63, "vmcnt range");
@@ -516,7 +519,8 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #pragma unroll
   for (int j = 0; j < LWB; ++j) {
     const uint32_t e = (uint32_t)((wave * LWB + j) * 64 + lane) * PW;
-    const uint32_t r = e / WPM, c = e - r * WPM;
+    const uint32_t r = e / WPM, q = e - r * WPM;
+    const uint32_t c = PSL ? (q % WS) * S + q / WS : q;  // PSL: LDS position q holds column c
     const int x = (int)c - (int)pxa;
     srow[j] = ((r < (uint32_t)RIN) & ((uint32_t)x < p.W)) ? r : 0xffffu;
     srel[j] = (r * p.W + (uint32_t)x) * 4u;
@@ -567,6 +571,50 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
     if (ic_issue == 0) plan_tile(i_issue);  // wave-uniform
     const float *const Ab = wres + ic * WREGC + kh * KK2 * OCT + li;
     const char *const Sb = (const char *)(ring + slot * SREG);
+    if constexpr (PSL) {
+      // phase-split strip (dc_kernel): one per-lane base per distinct half-1 shift, every fragment read
+      // base[kind(s)] + an immediate, the 32 pixels of a lane half on 32 consecutive dwords
+      using PK = dc_pkinds<KY, KX, S, WPM>;
+      constexpr int NK = PK::tab.nk;
+      asm volatile("" : "+v"(hsel));
+      const char *bs[NK];
+      dc_static_for<0, NK>([&](auto kc) {
+        constexpr int dkv = PK::tab.dk[decltype(kc)::value];
+        bs[decltype(kc)::value] = Sb + poff + (int)(hsel & (uint32_t)(dkv * 4));
+      });
+      auto fragp = [&](auto sc, float(&a)[TM], float &b) {
+        constexpr int s = decltype(sc)::value;
+        constexpr int k0 = dc_koffp<KX, S, WPM>(s, KK) * 4, kind = PK::tab.kind[s];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) a[t] = (DBG & 32) ? (float)(s + t) : Ab[s * OCT + 32 * t];
+        b = (DBG & 16) ? (float)s : *(const float *)(bs[kind] + k0);
+      };
+      float a[PF + 1][TM], b[PF + 1];
+      dc_static_for<0, PF>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s < KK2) fragp(sc, a[s], b[s]);
+      });
+      dc_static_for<0, KK2>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s + PF < KK2) fragp(std::integral_constant<int, s + PF>{}, a[(s + PF) % (PF + 1)], b[(s + PF) % (PF + 1)]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          if constexpr ((DBG & 2) != 0) acc[t][s % 16] += b[s % (PF + 1)] * a[s % (PF + 1)][t];
+          else acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[s % (PF + 1)], a[s % (PF + 1)][t], acc[t], 0, 0, 0);
+        }
+        if constexpr ((DBG & 1) == 0) {
+#pragma unroll
+          for (int q = (s * LWB + IS - 1) / IS; q < ((s + 1) * LWB + IS - 1) / IS && q < LWB; ++q) issue_one(q, islot, ic_issue);
+        }
+        if (dstores) {
+#pragma unroll
+          for (int q = (s * NST + ISS - 1) / ISS; q < ((s + 1) * NST + ISS - 1) / ISS && q < NST; ++q) store_one(q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      return;
+    }
     // lane half 1 reads tap KK2 + s where half 0 reads tap s: three per-lane bases (dc_kernel)
     constexpr int CSH = KK2 % KX, RSH = KK2 / KX;
     constexpr int DLO = RSH * WPM + CSH, DHI = (RSH + 1) * WPM + CSH - KX;
@@ -635,7 +683,7 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
     {
       const uint32_t px = p0 + (uint32_t)(wave * 32 + li);
       const uint32_t oy = fdiv(px, p.ow_m, p.ow_s), ox = px - oy * p.OW;
-      poff = px < p.OHW ? ((oy - oy_a) * S * WPM + ox * S + pxa - p.px) * 4u : 0u;
+      poff = px < p.OHW ? ((oy - oy_a) * S * WPM + (PSL ? ox : ox * S) + pxa - p.px) * 4u : 0u;
     }
 #pragma unroll
     for (int t = 0; t < TM; ++t)
@@ -701,10 +749,11 @@ __global__ __launch_bounds__(NW * 64) void dcr_kernel(GemmArgs p) {
 #endif
 }
 
-template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0>
+template <int KY, int KX, int S, int WPM, int RIN, int TM, int NW, int D, int V4, int ICMAX, int DBG = 0, int PFO = 0,
+          int PSL = 0>
 cfg_t dcr_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * NW, 2 * ((KY * KX + 1) / 2), 64 * NW, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = dcr_kernel<KY, KX, S, WPM, RIN, TM, NW, D, V4, ICMAX, DBG, PFO>;
+  c.k[A_KVEC][B_DIRECT][0] = dcr_kernel<KY, KX, S, WPM, RIN, TM, NW, D, V4, ICMAX, DBG, PFO, PSL>;
   c.dc_ci = V4;
   c.dc = 1;
   c.dc_ky = KY;
@@ -780,6 +829,10 @@ std::vector<cfg_t> dc_cfgs() {
       dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 0, 6>("dc7s2r32d3vf6"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 0, 8>("dc7s2r32d3vf8"),
       dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 0, 6>("dc11s4r32d2f6"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 1, 3, 0, 6>("dc11s4r32d2vf6"),
       dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 0, 8>("dc11s4r32d2f8"),
+      // phase-split strip (round 6): the B fragment reads of a lane half on 32 consecutive dwords
+      dcr_cfg<11, 11, 4, 228, 31, 1, 8, 2, 0, 3, 0, 0, 1>("dc11s4r32d2p"), dcr_cfg<11, 11, 4, 228, 31, 1, 8, 3, 0, 3, 0, 0, 1>("dc11s4r32d3p"),
+      dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 0, 3, 0, 0, 1>("dc7s2r32d3p"), dcr_cfg<7, 7, 2, 236, 13, 2, 8, 2, 0, 3, 0, 0, 1>("dc7s2r64d2p"),
+      dcr_cfg<7, 7, 2, 236, 13, 2, 8, 3, 0, 3, 0, 0, 1>("dc7s2r64d3p"),
 #ifdef BH_KTRACE
       // diagnostic forms of dc7s2r32d3v / dc11s4r32d2 (wrong results by design; tools/job_dcrdiag.sh)
       dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 1>("xdc7r_nodma"), dcr_cfg<7, 7, 2, 236, 13, 1, 8, 3, 1, 3, 2>("xdc7r_nomfma"),

@@ -373,6 +373,8 @@ struct cfg_t {
   int ref64 = 0;      // double-accumulating known-good kernel (bh_ref64.hip), never tuned in
   int k1n = 0;        // dc == 3: the pixels-on-N form (bh_k1s.hip k1n_kernel; gv_cx pixels per lane)
   int k1d = 0;        // dc == 3: the whole bank resident, input by 16-B LDS-DMA (bh_k1s.hip k1d_kernel)
+  int k1w = 0;        // dc == 3: store waves of the k1w form (bh_k1s.hip k1w_kernel; NT counts them too)
+  int k1w_sl = 0;     // k1w: LDS staging slots per compute wave
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and

@@ -296,7 +296,8 @@ __device__ __forceinline__ void stv(typename fvec<TN>::t v, __amdgpu_buffer_rsrc
                                            soff, AUX);
 }
 
-template <int TM, int TN, int KC, int Q, int NW>
+// DBG (instrumented library only, wrong results by design): bit 0 = the epilogue's stores dropped (OOB)
+template <int TM, int TN, int KC, int Q, int NW, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
   constexpr int OCT = 32 * TM;           // output channels of the block
   constexpr int UPX = 32 * TN;           // pixels per unit
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(NW * 64) void k1n_kernel(GemmArgs p) {
     const uint32_t so0 = oc0 * h4;
     const uint32_t n = pu * UPX + TN * li;
     const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
-    const uint32_t ob = oob_unless((pu < npu) & (n < p.N), (img * p.OCOHW + pix) * 4u + (uint32_t)(4 * kh) * h4);
+    const uint32_t ob = (DBG & 1) ? OOB : oob_unless((pu < npu) & (n < p.N), (img * p.OCOHW + pix) * 4u + (uint32_t)(4 * kh) * h4);
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -730,10 +731,218 @@ cfg_t k1d_cfg(const char *name) {
   return c;
 }
 
-template <int TM, int TN, int KC, int Q, int NW>
+// k1w_kernel (round 6, configs kw<OCT>c<KC>q<Q>w<NW>s<NSW>l<NSL>): k1n (TN = 1) with the output stores moved to
+// NSW store waves. vmcnt counts a wave's loads, LDS-DMAs and stores in issue order, so in k1n a wait for
+// an input chunk issued after a unit's epilogue also waits for that epilogue's 16 TM stores to complete
+// (round-3 diagnostics of k1s on 20x96x54^2 -> 96: 20.0 us with stores, 14.2 us with them dropped). Here a
+// compute wave never stores: it writes its finished unit [OCT][32] (biases included) into one of its NSL
+// LDS staging slots and bumps a counter; a store wave reads the slot back (ds_read_b128: 8 rows x 128 B per
+// instruction), adds the residual, applies the ReLU and issues 16-B stores (OH*OW % 4 == 0), and frees
+// the slot once its reads have returned -- it never waits for its stores. The compute waves' vmcnt then
+// holds only input loads: every chunk waits (Q - 2) KC / 2 loads deep. The bank slice is DMA'd whole in
+// the prologue (one barrier); after it no barrier runs, the hand-off is two LDS counters per compute wave
+// (data writes drained by lgkmcnt before the counter write; the reader branches on the counter before it
+// reads the data). Every spin is bounded (a hand-off that never comes ends the wave instead of hanging).
+template <int TM, int KC, int Q, int NW, int NSW, int NSL>
+__global__ __launch_bounds__((NW + NSW) * 64) void k1w_kernel(GemmArgs p) {
+  constexpr int OCT = 32 * TM, SC = KC / 2, PF = 3, TILE = OCT * 32, NT = (NW + NSW) * 64;
+  constexpr int BREG = ((OCT + 63) / 64) * 64;
+  constexpr uint32_t SPIN = 1u << 20;
+  static_assert(TM >= 1 && TM <= 3 && KC % 2 == 0 && SC % (PF + 1) == 0, "tile");
+  static_assert(Q >= 2 && (Q - 1) * SC <= 63, "vmcnt range");
+  static_assert(NW % NSW == 0 && NSW >= 1, "store waves serve whole groups of compute waves");
+  static_assert(NSL == 1 || NSL == 2, "staging slots per compute wave");
+  // [K][OCT] bank (padded to whole 64-lane 16-B DMAs), biases, staging [NW][NSL][OCT][32], counters full / done
+  extern __shared__ __attribute__((aligned(16))) float wl[];
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t l8 = blockIdx.x >> 3;
+  const uint32_t oct = l8 % p.tiles_m;
+  const uint32_t gi = (l8 / p.tiles_m) * 8 + (blockIdx.x & 7);
+  const uint32_t wg = (gridDim.x / p.tiles_m) * NW;  // compute waves per OC tile
+  const uint32_t oc0 = oct * OCT;
+  const uint32_t npu = (p.N + 31) / 32, nch = p.K / KC;
+  const uint32_t np = p.K * OCT / 4, lds_w = (np + 63) / 64 * 256;
+  const uint32_t hw4 = p.HW * 4u, ohw4 = p.OHW * 4u;
+  float *const bl = wl + lds_w;
+  float *const stg = bl + BREG;
+  volatile uint32_t *const full = (volatile uint32_t *)(stg + NW * NSL * TILE);
+  volatile uint32_t *const done = full + NW;
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsx = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+
+  if (tid < 2 * NW) full[tid] = 0u;  // full and done (before the prologue barrier)
+  // the whole bank slice [K][OCT]: piece e = (row e / (OCT / 4), columns oc0 + 4 (e % (OCT / 4)))
+  for (uint32_t e0 = (uint32_t)wave * 64; e0 < np; e0 += NT) {
+    const uint32_t e = e0 + (uint32_t)lane, r = e / (OCT / 4), q = e % (OCT / 4);
+    dma16(rsw, wl + 4 * e0, oob_unless((e < np) & (oc0 + 4 * q < p.lda), (r * p.lda + oc0 + 4 * q) * 4u));
+  }
+  if (64 * wave < BREG) dma4(rsbias, bl + 64 * wave, oob_unless(oc0 + 64 * wave + lane < p.M, (oc0 + 64 * wave + lane) * 4u));
+
+  if (wave >= NW) {  // ---- store wave: serves compute waves w = sw, sw + NSW, ...
+    vm_wait<0>();
+    __syncthreads();
+    const int sw = wave - NW;
+    constexpr int NS = NW / NSW;
+    uint32_t cnt[NS], dn[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const uint32_t pu0 = gi * NW + (uint32_t)(sw + k * NSW);
+      cnt[k] = pu0 < npu ? (npu - pu0 + wg - 1) / wg : 0u;
+      dn[k] = 0;
+    }
+    const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+    const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+    const float floor0 = p.relu ? 0.0f : __builtin_nanf("");  // relu_floor: NaN = no clamp
+    const uint32_t rl = (uint32_t)lane >> 3, cq = 4u * ((uint32_t)lane & 7u);  // row in a group of 8, first pixel
+    for (uint32_t spin = 0; spin < SPIN;) {
+      bool all = true, prog = false;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        if (dn[k] >= cnt[k]) continue;
+        all = false;
+        const int w = sw + k * NSW;
+        if (full[w] <= dn[k]) continue;
+        prog = true;
+        asm volatile("" ::: "memory");  // the slot's reads stay behind the counter's
+        const uint32_t j = dn[k], pu = gi * NW + (uint32_t)w + j * wg;
+        const float *const tile = stg + (w * NSL + (int)(j % NSL)) * TILE + (rl * 32 + cq);
+        f32x4v v[OCT / 8];
+#pragma unroll
+        for (int g = 0; g < OCT / 8; ++g) v[g] = *(const f32x4v *)(tile + g * 8 * 32);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        done[w] = j + 1;  // the slot's data is in registers
+        dn[k] = j + 1;
+        const uint32_t n = pu * 32u + cq;
+        const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+        const uint32_t ob = (img * p.OCOHW + pix) * 4u + rl * ohw4;
+#pragma unroll
+        for (int g = 0; g < OCT / 8; ++g) {
+          const uint32_t oc = oc0 + (uint32_t)(8 * g) + rl, so = (oc0 + (uint32_t)(8 * g)) * ohw4;
+          const uint32_t o = oob_unless((oc < p.M) & (n < p.N), ob);
+          f32x4v x = v[g];
+          if (p.res) x += ldv<4>(rsr, o, so);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = relu_floor(x[e], floor0);
+          if (p.wt) stv<4, AUX_SC1>(x, rso, o, so);
+          else stv<4, AUX_OUT>(x, rso, o, so);
+        }
+      }
+      if (all) break;
+      if (!prog) {
+        __builtin_amdgcn_s_sleep(1);
+        ++spin;
+      }
+    }
+    return;
+  }
+
+  // ---- compute wave: k1n's stream (TN = 1), no stores
+  auto ubase = [&](uint32_t pu) -> uint32_t {
+    const uint32_t n = pu * 32u + (uint32_t)li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    return oob_unless((pu < npu) & (n < p.N), (img * p.ICHW + pix + kh * p.HW) * 4u);
+  };
+  float xr[Q][SC];
+  auto issue = [&](int q, uint32_t base, uint32_t c) {
+    const uint32_t vb = base + c * KC * hw4;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) xr[q][s] = ldv<1>(rsx, vb, 2 * s * hw4);
+  };
+  uint32_t pu = gi * NW + (uint32_t)wave;
+  uint32_t bcur = ubase(pu), bnext = ubase(pu + wg);
+#pragma unroll
+  for (int q = 0; q < Q - 1; ++q) issue(q, bcur, (uint32_t)q);
+  vm_wait<(Q - 2) * SC>();  // the bank, the biases and chunk 0 (this wave's)
+  __syncthreads();          // every wave's bank DMAs
+  if (pu >= npu) return;
+
+  f32x16 acc[TM];
+  float wf[PF + 1][TM];
+  const float *const wb = wl + kh * OCT + li;
+  auto frag = [&](float (&w)[TM], uint32_t c, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) w[t] = wb[(c * KC + 2 * s) * OCT + 32 * t];
+  };
+  f32x16 biasv[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4v b4 = *(const f32x4v *)(bl + 32 * t + 8 * g + 4 * kh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) biasv[t][4 * g + e] = b4[e];
+    }
+  auto chunk = [&](int r, uint32_t cq, bool first) {
+    vm_wait<(Q - 2) * SC>();  // (a no-op on the first unit's chunk 0)
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const uint32_t c2 = cq + (uint32_t)(r + Q - 1);
+      const bool nx = c2 >= nch;
+      issue((r + Q - 1) % Q, nx ? bnext : bcur, nx ? c2 - nch : c2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t c = cq + (uint32_t)r, cn = c + 1 == nch ? 0u : c + 1;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {
+      if (s + PF < SC) frag(wf[(s + PF) % (PF + 1)], c, s + PF);
+      else frag(wf[(s + PF) % (PF + 1)], cn, s + PF - SC);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s % (PF + 1)][t], xr[r % Q][s],
+                                                       first && r == 0 && s == 0 ? biasv[t] : acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < PF; ++s) frag(wf[s], 0, s);
+  for (uint32_t j = 0;; ++j) {
+#pragma unroll
+    for (int r = 0; r < Q; ++r) chunk(r, 0, true);
+    for (uint32_t cq = Q; cq < nch; cq += Q) {
+#pragma unroll
+      for (int r = 0; r < Q; ++r) chunk(r, cq, false);
+    }
+    // hand the unit to the store wave: slot j % NSL once the store wave has read unit j - NSL out of it
+    for (uint32_t spin = 0; j - done[wave] >= (uint32_t)NSL && spin < SPIN; ++spin) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    float *const st = stg + (wave * NSL + (int)(j % NSL)) * TILE + (4 * kh) * 32 + li;
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[(32 * t + 8 * g + i) * 32] = acc[t][4 * g + i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    full[wave] = j + 1;
+    pu += wg;
+    if (pu >= npu) break;
+    bcur = bnext;
+    bnext = ubase(pu + wg);
+  }
+  vm_wait<0>();
+}
+
+template <int TM, int KC, int Q, int NW, int NSW, int NSL>
+cfg_t k1w_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * NW, KC, 64 * (NW + NSW), {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = k1w_kernel<TM, KC, Q, NW, NSW, NSL>;
+  c.dc = 3;
+  c.dc_ky = 1;
+  c.dc_kx = 1;
+  c.dc_ci = KC;
+  c.dc_rin = Q;
+  c.k1w = NSW;
+  c.k1w_sl = NSL;
+  return c;
+}
+
+template <int TM, int TN, int KC, int Q, int NW, int DBG = 0>
 cfg_t k1n_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * TN * NW, KC, 64 * NW, {}, 1};
-  c.k[A_KVEC][B_DIRECT][0] = k1n_kernel<TM, TN, KC, Q, NW>;
+  c.k[A_KVEC][B_DIRECT][0] = k1n_kernel<TM, TN, KC, Q, NW, DBG>;
   c.dc = 3;
   c.dc_ky = 1;
   c.dc_kx = 1;
@@ -788,8 +997,16 @@ std::vector<cfg_t> k1s_cfgs() {
       k1d_cfg<3, 32, 4, 4>("kd96c32d4w4"), k1d_cfg<3, 16, 7, 4>("kd96c16d7w4"), k1d_cfg<2, 32, 3, 4>("kd64c32d3w4"),
       k1d_cfg<2, 16, 5, 4>("kd64c16d5w4"), k1d_cfg<2, 32, 3, 8>("kd64c32d3w8"), k1d_cfg<1, 32, 4, 4>("kd32c32d4w4"),
       k1d_cfg<1, 32, 3, 8>("kd32c32d3w8"),
+      // k1w <TM, KC, Q, NW, NSW, NSL>: kw<OC tile>c<KC>q<Q>w<compute waves>s<store waves>l<staging slots>
+      k1w_cfg<1, 32, 3, 8, 2, 2>("kw32c32q3w8s2l2"), k1w_cfg<1, 16, 4, 8, 2, 2>("kw32c16q4w8s2l2"),
+      k1w_cfg<1, 16, 3, 8, 2, 2>("kw32c16q3w8s2l2"), k1w_cfg<1, 16, 4, 4, 1, 2>("kw32c16q4w4s1l2"),
+      k1w_cfg<2, 16, 4, 4, 1, 2>("kw64c16q4w4s1l2"), k1w_cfg<2, 16, 4, 8, 2, 1>("kw64c16q4w8s2l1"),
+      k1w_cfg<2, 8, 4, 8, 2, 1>("kw64c8q4w8s2l1"),   k1w_cfg<3, 8, 4, 4, 1, 1>("kw96c8q4w4s1l1"),
+      k1w_cfg<3, 16, 3, 4, 1, 1>("kw96c16q3w4s1l1"),
 #ifdef BH_KTRACE
       k1d_cfg<3, 32, 4, 4, 1>("xkd96c32d4w4_nostore"), k1d_cfg<3, 16, 6, 4, 1>("xkd96c16d6w4_nostore"),
+      k1n_cfg<1, 1, 32, 3, 8, 1>("xkn32p32c32q3w8_nostore"), k1n_cfg<1, 1, 16, 4, 8, 1>("xkn32p32c16q4w8_nostore"),
+      k1n_cfg<3, 2, 8, 4, 4, 1>("xkn96p64c8q4w4_nostore"),
 #endif
 #ifdef BH_KTRACE
       k1s_cfg<3, 32, 3, 4, 1>("xks96c32q3_noload"), k1s_cfg<3, 32, 3, 4, 2>("xks96c32q3_nomfma"),
@@ -853,6 +1070,9 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   if (c.k1d) return launch_k1d(ctx, c, p, splits, first);
   if (p.K % KC || (p.K / KC) % Q)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a whole number of ") + c.name + " trips");
+  // k1w: a store-wave lane's 4 pixels lie in one image and its 16-B output / residual accesses are aligned
+  if (c.k1w && (p.OHW % 4 || (uintptr_t)p.c % 16 || (uintptr_t)p.res % 16))
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs OH*OW % 4 == 0 and 16-B aligned output rows");
   // k1n: a lane's gv_cx pixels lie in one image (OH*OW % gv_cx == 0) and its vector loads / stores
   // are aligned
   const uint32_t tn = (uint32_t)c.gv_cx;
@@ -862,8 +1082,13 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
                                   " == 0 and aligned input / output rows");
   // k1s: the bank slice [IC][OCT] and one [32][36] epilogue staging tile per wave; k1n: the bank
   // slice and the tile's biases (whole 64-float DMAs)
-  const uint64_t lds = c.k1n ? ((uint64_t)p.K * c.BM + (uint64_t)((c.BM + 63) / 64) * 64) * 4
-                             : ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;
+  // k1w: the bank slice padded to whole 64-lane 16-B DMAs, the biases, c.k1w_sl [BM][32] staging slots per
+  // compute wave and two counters per compute wave
+  const uint32_t nw = NT / 64 - (uint32_t)c.k1w;  // compute waves
+  const uint64_t lds = c.k1w  ? (((uint64_t)p.K * c.BM / 4 + 63) / 64 * 256 + (uint64_t)((c.BM + 63) / 64) * 64 +
+                                (uint64_t)nw * c.k1w_sl * c.BM * 32 + 2 * nw) * 4
+                       : c.k1n ? ((uint64_t)p.K * c.BM + (uint64_t)((c.BM + 63) / 64) * 64) * 4
+                               : ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;
   if (lds > 160 * 1024) return bh::fail(BH_UNSUP, std::string("conv: bank slice too large for ") + c.name);
   const uint64_t out_bytes = (uint64_t)p.OCOHW * (p.N / p.OHW) * 4;
   if (out_bytes >= 0x7fffff00ull) return bh::fail(BH_UNSUP, "conv: output too large for the k1s kernel");
@@ -874,7 +1099,7 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, c.NT, (size_t)lds) != hipSuccess || occ < 1) occ = 1;
   const uint32_t oct = (p.M + c.BM - 1) / c.BM;
-  const uint32_t npu = (p.N + 32 * (c.k1n ? tn : 1u) - 1) / (32 * (c.k1n ? tn : 1u)), nw = NT / 64;
+  const uint32_t npu = (p.N + 32 * (c.k1n ? tn : 1u) - 1) / (32 * (c.k1n ? tn : 1u));
   const bool full = splits >= 8;
   uint32_t bpc = splits && !full ? splits : 2;
   bpc = std::max(1u, std::min<uint32_t>(bpc, (uint32_t)std::min(occ, 4)));

@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = [("kn32p32c32q3w8", ops.ConvShape(2, 96, 14, 14, 96, 1, 1, 1, 1, 0, 0)),
          ("kn64p64c16q3w8", ops.ConvShape(2, 96, 12, 12, 72, 1, 1, 1, 1, 0, 0)),
+         ("kw32c16q3w8s2l2", ops.ConvShape(2, 96, 14, 14, 96, 1, 1, 1, 1, 0, 0)),
          ("dc7s2r32d3v", ops.ConvShape(2, 3, 224, 224, 64, 7, 7, 2, 2, 3, 3)),
          ("dc11s4r32d2", ops.ConvShape(1, 3, 227, 227, 96, 11, 11, 4, 4, 0, 0))]
 
