@@ -328,7 +328,8 @@ __device__ __forceinline__ void staged_epilogue(float *lds, f32x16 (&acc)[TM][TN
 }
 
 // max(x, floor) as one v_max_f32 (fmaxf adds a canonicalizing v_max per operand in IEEE mode);
-// floor is 0 (ReLU) or -inf (none), wave-uniform; the accumulators hold no NaN of interest to quiet
+// floor is 0 (ReLU) or a quiet NaN (none: v_max_f32 returns the other operand, so x passes as is, a NaN
+// included), wave-uniform
 __device__ __forceinline__ float relu_floor(float x, float floor) {
   float r;
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(floor), "v"(x));

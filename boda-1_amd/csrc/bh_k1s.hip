@@ -987,6 +987,9 @@ std::vector<cfg_t> k1s_cfgs() {
       k1n_cfg<2, 2, 16, 4, 4>("kn64p64c16q4w4"),   k1n_cfg<3, 1, 8, 4, 8>("kn96p32c8q4w8"),
       k1n_cfg<3, 2, 8, 4, 8>("kn96p64c8q4w8"),     k1n_cfg<3, 2, 16, 2, 8>("kn96p64c16q2w8"),
       k1n_cfg<3, 2, 8, 4, 4>("kn96p64c8q4w4"),
+      // round 6: a unit's whole K (96) in flight, the ring waits never short of loads
+      k1n_cfg<1, 1, 8, 12, 8>("kn32p32c8q12w8"),   k1n_cfg<1, 1, 16, 6, 8>("kn32p32c16q6w8"),
+      k1n_cfg<1, 1, 16, 6, 4>("kn32p32c16q6w4"),
       // k1d <TM, KC, D, NW>: kd<OC sub-tile>c<KC>d<ring slots>w<NW>, the whole bank resident
       k1d_cfg<3, 16, 6, 4>("kd96c16d6w4"), k1d_cfg<3, 16, 8, 4>("kd96c16d8w4"), k1d_cfg<3, 16, 5, 8>("kd96c16d5w8"),
       k1d_cfg<2, 16, 6, 4>("kd64c16d6w4"), k1d_cfg<2, 16, 8, 4>("kd64c16d8w4"), k1d_cfg<2, 16, 5, 8>("kd64c16d5w8"),
@@ -1003,6 +1006,8 @@ std::vector<cfg_t> k1s_cfgs() {
       k1w_cfg<2, 16, 4, 4, 1, 2>("kw64c16q4w4s1l2"), k1w_cfg<2, 16, 4, 8, 2, 1>("kw64c16q4w8s2l1"),
       k1w_cfg<2, 8, 4, 8, 2, 1>("kw64c8q4w8s2l1"),   k1w_cfg<3, 8, 4, 4, 1, 1>("kw96c8q4w4s1l1"),
       k1w_cfg<3, 16, 3, 4, 1, 1>("kw96c16q3w4s1l1"),
+      k1w_cfg<3, 8, 12, 4, 1, 1>("kw96c8q12w4s1l1"), k1w_cfg<3, 16, 6, 4, 1, 1>("kw96c16q6w4s1l1"),
+      k1w_cfg<1, 8, 12, 8, 2, 2>("kw32c8q12w8s2l2"),
 #ifdef BH_KTRACE
       k1d_cfg<3, 32, 4, 4, 1>("xkd96c32d4w4_nostore"), k1d_cfg<3, 16, 6, 4, 1>("xkd96c16d6w4_nostore"),
       k1n_cfg<1, 1, 32, 3, 8, 1>("xkn32p32c32q3w8_nostore"), k1n_cfg<1, 1, 16, 4, 8, 1>("xkn32p32c16q4w8_nostore"),
