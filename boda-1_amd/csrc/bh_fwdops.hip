@@ -62,6 +62,92 @@ __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in,
   (void)C;
 }
 
+// Pooling staged through LDS (round 6), used for the windows pool_kernel loops over at run time
+// (global pooling: 49 dependent-address taps per thread there). pool_kernel reads every tap
+// straight from global memory: lanes S floats apart, KY*KX dword loads per output. Here a
+// block copies a band of whole input rows -- or several whole planes when a plane is small -- into
+// LDS with coalesced loads (each input float read once, plus KY - sy overlap rows per band), then
+// computes the band's outputs from LDS in pool_kernel's tap order (kx outer, ky inner: the same
+// max / argmax ties and the same average summation order, so the results are bitwise the same).
+// Block = (plane group of PPB planes, output row band of RB rows); PPB > 1 only when RB covers OH.
+constexpr int POOL_LDS = 8192;  // floats of input staged per block
+template <int KY_, int KX_>
+__global__ __launch_bounds__(256) void pool_lds_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                       float *__restrict__ out_in_yx, uint32_t NC, uint32_t H,
+                                                       uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY_rt,
+                                                       uint32_t KX_rt, uint32_t sy, uint32_t sx, uint32_t py,
+                                                       uint32_t px, int avg, uint32_t RB, uint32_t PPB,
+                                                       uint32_t nbands, uint32_t ow_m, uint32_t ow_s, uint32_t oh_m,
+                                                       uint32_t oh_s) {
+  __shared__ float t[POOL_LDS];
+  const uint32_t KY = KY_ > 0 ? (uint32_t)KY_ : KY_rt, KX = KX_ > 0 ? (uint32_t)KX_ : KX_rt;
+  const uint32_t band = blockIdx.x % nbands, nc0 = (blockIdx.x / nbands) * PPB;
+  const uint32_t np = min(PPB, NC - nc0);
+  const uint32_t oy0 = band * RB, oy1 = min(OH, oy0 + RB);
+  // staged input rows [iy0, iy0 + rows): whole planes when PPB > 1 (then RB >= OH and the planes
+  // are one contiguous run), else the rows the band's windows touch, clipped to the image
+  int iy0 = 0, iy1 = (int)H;
+  if (PPB == 1) {
+    iy0 = max(0, (int)(oy0 * sy) - (int)py);
+    iy1 = min((int)H, (int)((oy1 - 1) * sy + KY) - (int)py);
+  }
+  const uint32_t rows = iy1 > iy0 ? (uint32_t)(iy1 - iy0) : 0u, per = rows * W, total = np * per;
+  const float *const src = in + (size_t)nc0 * H * W + (size_t)iy0 * W;
+  // all of a thread's loads in flight together, then the LDS writes (total <= POOL_LDS)
+  float r[POOL_LDS / 256];
+#pragma unroll
+  for (int j = 0; j < POOL_LDS / 256; ++j) {
+    const uint32_t e = threadIdx.x + 256u * j;
+    r[j] = e < total ? src[e] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < POOL_LDS / 256; ++j) {
+    const uint32_t e = threadIdx.x + 256u * j;
+    if (e < total) t[e] = r[j];
+  }
+  __syncthreads();
+  const uint32_t nrow = oy1 - oy0, nout = np * nrow * OW;
+  for (uint32_t o = threadIdx.x; o < nout; o += 256) {
+    const uint32_t q = (__umulhi(o, ow_m) + o) >> ow_s, ox = o - q * OW;  // q = plane * nrow + row
+    uint32_t pl = 0, ry = q;
+    if (PPB > 1) {  // nrow == OH
+      pl = (__umulhi(q, oh_m) + q) >> oh_s;
+      ry = q - pl * OH;
+    }
+    const uint32_t oy = oy0 + ry;
+    const float *const T = t + pl * per;
+    float v = avg ? 0.0f : -FLT_MAX, cnt = 0.0f;
+    int oyx = -1;
+    auto tap = [&](uint32_t ky, uint32_t kx) {
+      const int iy = (int)(oy * sy + ky) - (int)py, ix = (int)(ox * sx + kx) - (int)px;
+      const bool ok = iy >= 0 && ix >= 0 && ix < (int)W && iy < (int)H;
+      const float x = T[ok ? (iy - iy0) * (int)W + ix : 0];
+      if (ok) {
+        if (avg) {
+          v += x;
+          cnt += 1.0f;
+        } else if (x > v) {
+          v = x;
+          oyx = iy * (int)W + ix;
+        }
+      }
+    };
+    if constexpr (KY_ > 0 && KX_ > 0) {
+#pragma unroll
+      for (int kx = 0; kx < KX_; ++kx)
+#pragma unroll
+        for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
+    } else {
+      for (uint32_t kx = 0; kx < KX; ++kx)
+        for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
+    }
+    if (avg) v /= cnt;
+    const size_t i = ((size_t)(nc0 + pl) * OH + oy) * OW + ox;
+    out[i] = v;
+    if (out_in_yx) out_in_yx[i] = (float)oyx;
+  }
+}
+
 // LRN across channels (test/rtc/lrn.cucl, LRN_MATCH_CAFFE): a running sum of squares over a
 // window of LS channels kept with a ring of the last LS inputs (+ new^2 - old^2, the
 // reference's order), out = in * (k + alpha/LS * sum)^-beta.
@@ -243,6 +329,30 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
   uint32_t tot = (uint32_t)total;
   const fastdiv fow = make_fastdiv(OW), foh = make_fastdiv(OH);
   uint32_t ow_m = fow.m, ow_s = fow.s, oh_m = foh.m, oh_s = foh.s;
+  // the LDS-staged form for the windows without a compile-time kernel (global / large windows: the
+  // googlenet 7x7 average pool 10.7 -> 8.2 us at batch 20), where a band of at least one output row
+  // fits POOL_LDS floats: whole planes (PPB of them, at least 512 blocks where there are enough
+  // planes) when a plane fits, else bands of RB output rows of one plane. On the 3x3 and 2x2 pools
+  // it measured slower than pool_kernel (googlenet pool1 31.7 -> 34.9 us, inception 3x3 s1 15.0 ->
+  // 27.6 us, VGG pool2 37.0 -> 40.8 us; profiles/r06/layers/): those keep the global-memory form
+  uint32_t NC = B * C, RB = 0, PPB = 1, nbands = 1;
+  const bool fixed = (KY == 3 && KX == 3) || (KY == 2 && KX == 2);
+  if (fixed) {
+  } else if ((uint64_t)H * W <= (uint64_t)POOL_LDS) {
+    RB = OH;
+    PPB = std::max(1u, std::min<uint32_t>((uint32_t)POOL_LDS / (H * W), NC / 512));
+  } else if (W <= (uint32_t)POOL_LDS && (uint32_t)POOL_LDS / W >= KY) {
+    RB = std::min(OH, ((uint32_t)POOL_LDS / W - KY) / sy + 1);
+    nbands = (OH + RB - 1) / RB;
+  }
+  if (RB) {
+    const uint64_t blocks = (uint64_t)((NC + PPB - 1) / PPB) * nbands;
+    if (blocks < (1ull << 31)) {
+      void *la[] = {&in, &out, &out_in_yx, &NC, &H, &W, (void *)&OH, (void *)&OW, &KY, &KX, &sy, &sx, &py, &px,
+                    &avg, &RB, &PPB, &nbands, &ow_m, &ow_s, &oh_m, &oh_s};
+      return launch(ctx, (const void *)pool_lds_kernel<0, 0>, dim3((uint32_t)blocks), dim3(256), la, true, true, "pool");
+    }
+  }
   void *args[] = {&in,  &out, &out_in_yx, &tot, &C,   &H,   &W,   (void *)&OH, (void *)&OW, &KY,
                   &KX,  &sy,  &sx,        &py,  &px,  &avg, &ow_m, &ow_s,      &oh_m,       &oh_s};
   const void *kern = KY == 3 && KX == 3   ? (const void *)pool_kernel<3, 3>

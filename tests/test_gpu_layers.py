@@ -32,6 +32,14 @@ POOLS = [  # B, C, H, W, KY, KX, sy, sx, py, px, avg
     (2, 5, 40, 37, 3, 3, 1, 1, 1, 1, 1),     # wide rows: padded average, stride 1
     (2, 3, 30, 41, 2, 2, 2, 2, 0, 0, 0),     # 2x2 (VGG-style), partial last column
     (1, 2, 19, 70, 5, 4, 3, 3, 2, 1, 0),     # runtime window, partial last row
+    (2, 8, 112, 112, 3, 3, 2, 2, 0, 0, 0),   # GoogLeNet pool1 plane
+    (1, 4, 224, 224, 2, 2, 2, 2, 0, 0, 0),   # VGG pool1 plane
+    # runtime windows: the LDS-staged kernel (bh_fwdops.hip pool_lds_kernel), its bands, plane groups
+    # and the fallback
+    (1, 3, 100, 100, 5, 5, 1, 1, 2, 2, 1),   # padded stride-1 average across band edges
+    (1, 2, 120, 120, 5, 4, 2, 3, 2, 1, 0),   # max with argmax across band edges
+    (2, 600, 6, 6, 6, 6, 1, 1, 0, 0, 1),     # global average, 2 planes per block
+    (1, 1, 4, 3000, 4, 4, 2, 2, 0, 0, 0),    # rows too wide for a band: the global-memory kernel
 ]
 
 

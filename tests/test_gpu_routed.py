@@ -48,6 +48,22 @@ for _p in [os.path.join(OPS, "op_sigs_full.txt")] + [os.path.join(TUNING, "net-o
             CONV.append(_s)
 
 
+def test_table_routes_are_the_ones_run(dev):
+    """Every table line's op runs its table configuration in this process (the table loaded, nothing
+    overriding it), so the route tests here and in test_gpu_conv.py check what the bench runs."""
+    wrong = []
+    for line in open(os.path.join(TUNING, "gfx950.tune")):
+        if line.startswith("#") or " cfg=" not in line:
+            continue
+        key, rest = line.split(" cfg=", 1)
+        op, dims = key.split()[0], [int(x) for x in key.split()[1:]]
+        cfg = rest.split()[0]
+        v = dev.variant(0 if op == "sgemm" else 1, dims)
+        if cfg not in v:
+            wrong.append((key, cfg, v))
+    assert not wrong, wrong[:10]
+
+
 @pytest.mark.parametrize("mnk", SGEMM, ids=lambda t: "x".join(map(str, t)))
 def test_sgemm_tuned_route_kat(dev, mnk):
     M, N, K = mnk

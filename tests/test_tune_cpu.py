@@ -64,3 +64,10 @@ def test_merge_deletes_entries(tmp_path):
     lines = [l for l in out.read_text().splitlines() if not l.startswith("#")]
     assert lines == ["conv 5 2 3 3 4 1 1 1 1 0 0 cfg=gvs16x16w8 splits=1 red=i",
                      "conv 20 2 3 3 4 1 1 1 1 0 0 cfg=kn32p32c32q3w8 splits=2 red=i wt=1"]
+
+
+def test_import_leaves_the_table_alone():
+    """Importing the tuner must not point BH_TUNE_FILE away from the committed table: pytest imports
+    this module while collecting, and every GPU test of the same process would then run the heuristic
+    routes instead of the table's (as one round-6 suite run did)."""
+    assert os.environ.get("BH_TUNE_FILE") != "/nonexistent"

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import boda_hip  # noqa: E402
 from boda_hip import ops, runner  # noqa: E402
-import tune  # noqa: E402  (sets BH_TUNE_FILE to nothing, for the tuner's own sweeps)
+import tune  # noqa: E402
 
 # "tuned" = the committed table's route (as in the bench), unless --no-table
 _TABLE = os.path.join(ROOT, "boda-1_amd", "tuning", "gfx950.tune")
@@ -34,8 +34,7 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--no-table", action="store_true", help="compare against the untuned heuristic")
     a = ap.parse_args()
-    if not a.no_table:
-        os.environ["BH_TUNE_FILE"] = _TABLE
+    os.environ["BH_TUNE_FILE"] = "/nonexistent" if a.no_table else _TABLE
     shapes = [ops.ConvShape(*map(int, c.split(","))) for c in a.conv]
     shapes += [ops.SgemmShape(*map(int, c.split(","))) for c in a.sgemm]
     if a.top:

@@ -18,8 +18,8 @@ from boda_hip import ops, runner  # noqa: E402
 _TUNE_ENV = os.environ.get("BH_TUNE_FILE")
 from tools.tune import time_op  # noqa: E402
 
-# tools.tune points BH_TUNE_FILE at nothing (it tunes against the heuristic); the "table"
-# candidate here means the committed table (or the caller's BH_TUNE_FILE)
+# the "table" candidate here means the committed table (or the caller's BH_TUNE_FILE); tools.tune
+# points BH_TUNE_FILE at nothing only in its own main()
 if _TUNE_ENV is None:
     os.environ.pop("BH_TUNE_FILE", None)
 else:

@@ -24,8 +24,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "boda-1_amd"))
 sys.path.insert(0, ROOT)
 
-# tune against the built-in heuristic, not against a previously committed table
-os.environ["BH_TUNE_FILE"] = "/nonexistent"
 import boda_hip  # noqa: E402
 from boda_hip import ops, runner  # noqa: E402
 
@@ -209,6 +207,10 @@ def main():
     ap.add_argument("--keep-prev", action="store_true", help="load the --out table's choices as with --cfg-re: "
                     "kept unless beaten by --min-gain")
     args = ap.parse_args()
+    # tune against the built-in heuristic, not against a previously committed table (set here, not at
+    # import: importing this module -- tests/test_tune_cpu.py, tools/cfgprobe.py -- must not change the
+    # route of every later call in the importing process; the table loads at the first conv / sgemm call)
+    os.environ["BH_TUNE_FILE"] = "/nonexistent"
     global TIMING
     TIMING = args.timing
 
