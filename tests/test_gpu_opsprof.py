@@ -109,11 +109,11 @@ def test_ops_prof_multi_tune_vs_kg(suite, outlier, tmp_path, golden):
     assert all(float(x[6]) == (2e-3 if "_wino_" in x[2] else 2e-4) for x in runs)  # digest tolerances
     print("max element difference from the kg tune per tune:",
           {t: max(float(x[3]) for x in runs if x[1] == t) for t in sorted({x[1] for x in runs})})
-    # tighter than the 2e-3 floor for the direct routes: the table's routes within test_gpu_conv's
-    # DIRECT_ELEM_TOL (1e-3), the forced tile / K-chunked kernels too (7.3e-4 / 4.6e-4 measured), the
-    # forced dm3 within 1.5e-3 (1.2e-3 at K = 3456, profiles/r05/route_acc_3x3.txt); the kg tune is the
-    # exact sum rounded once, so these are each route's own error
-    bound = {"tab": 1e-3, "tile": 1e-3, "gvs": 1e-3, "dm": 1.5e-3}
+    # tighter than the 2e-3 floor for the direct routes on this list (K <= 3456): the forced tile /
+    # K-chunked kernels within 1e-3 (7.3e-4 / 4.6e-4 measured), the table's routes and the forced dm3
+    # within 1.5e-3 (dm3 1.2e-3 at K = 3456, profiles/r05/route_acc_3x3.txt); the kg tune is the exact
+    # sum rounded once, so these are each route's own error
+    bound = {"tab": 1.5e-3, "tile": 1e-3, "gvs": 1e-3, "dm": 1.5e-3}
     over = [x for x in runs if x[1] in bound and "_wino_" not in x[2] and float(x[3]) > bound[x[1]]]
     assert not over, over
     bad = [x for x in runs if x[7] != "ok"]
