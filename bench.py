@@ -346,8 +346,8 @@ def main():
     if os.path.exists(rp):
         try:
             rj = json.load(open(rp))
-            units = sorted(r["dims"] for r in recs if r["variant"] == dom)
-            same = rj.get("units") == units and rj.get("build_hash") == build_hash()
+            dom_units = sorted(r["dims"] for r in recs if r["variant"] == dom)
+            same = rj.get("units") == dom_units and rj.get("build_hash") == build_hash()
             if rj.get("kernel") == dom and rj.get("avg_ns") and not same:
                 roof["frac_rocprof_stale"] = ("profiles/rocprof_dominant.json was measured on another build or "
                                               "other launches of this kernel: not reported")
