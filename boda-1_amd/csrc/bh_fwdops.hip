@@ -71,16 +71,13 @@ __global__ __launch_bounds__(256) void pool_kernel(const float *__restrict__ in,
 // max / argmax ties and the same average summation order, so the results are bitwise the same).
 // Block = (plane group of PPB planes, output row band of RB rows); PPB > 1 only when RB covers OH.
 constexpr int POOL_LDS = 8192;  // floats of input staged per block
-template <int KY_, int KX_>
 __global__ __launch_bounds__(256) void pool_lds_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                        float *__restrict__ out_in_yx, uint32_t NC, uint32_t H,
-                                                       uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY_rt,
-                                                       uint32_t KX_rt, uint32_t sy, uint32_t sx, uint32_t py,
-                                                       uint32_t px, int avg, uint32_t RB, uint32_t PPB,
-                                                       uint32_t nbands, uint32_t ow_m, uint32_t ow_s, uint32_t oh_m,
-                                                       uint32_t oh_s) {
+                                                       uint32_t W, uint32_t OH, uint32_t OW, uint32_t KY, uint32_t KX,
+                                                       uint32_t sy, uint32_t sx, uint32_t py, uint32_t px, int avg,
+                                                       uint32_t RB, uint32_t PPB, uint32_t nbands, uint32_t ow_m,
+                                                       uint32_t ow_s, uint32_t oh_m, uint32_t oh_s) {
   __shared__ float t[POOL_LDS];
-  const uint32_t KY = KY_ > 0 ? (uint32_t)KY_ : KY_rt, KX = KX_ > 0 ? (uint32_t)KX_ : KX_rt;
   const uint32_t band = blockIdx.x % nbands, nc0 = (blockIdx.x / nbands) * PPB;
   const uint32_t np = min(PPB, NC - nc0);
   const uint32_t oy0 = band * RB, oy1 = min(OH, oy0 + RB);
@@ -132,15 +129,8 @@ __global__ __launch_bounds__(256) void pool_lds_kernel(const float *__restrict__
         }
       }
     };
-    if constexpr (KY_ > 0 && KX_ > 0) {
-#pragma unroll
-      for (int kx = 0; kx < KX_; ++kx)
-#pragma unroll
-        for (int ky = 0; ky < KY_; ++ky) tap(ky, kx);
-    } else {
-      for (uint32_t kx = 0; kx < KX; ++kx)
-        for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
-    }
+    for (uint32_t kx = 0; kx < KX; ++kx)
+      for (uint32_t ky = 0; ky < KY; ++ky) tap(ky, kx);
     if (avg) v /= cnt;
     const size_t i = ((size_t)(nc0 + pl) * OH + oy) * OW + ox;
     out[i] = v;
@@ -350,7 +340,7 @@ int launch_pool(bh_ctx *ctx, const float *in, float *out, float *out_in_yx, uint
     if (blocks < (1ull << 31)) {
       void *la[] = {&in, &out, &out_in_yx, &NC, &H, &W, (void *)&OH, (void *)&OW, &KY, &KX, &sy, &sx, &py, &px,
                     &avg, &RB, &PPB, &nbands, &ow_m, &ow_s, &oh_m, &oh_s};
-      return launch(ctx, (const void *)pool_lds_kernel<0, 0>, dim3((uint32_t)blocks), dim3(256), la, true, true, "pool");
+      return launch(ctx, (const void *)pool_lds_kernel, dim3((uint32_t)blocks), dim3(256), la, true, true, "pool");
     }
   }
   void *args[] = {&in,  &out, &out_in_yx, &tot, &C,   &H,   &W,   (void *)&OH, (void *)&OW, &KY,
