@@ -376,6 +376,7 @@ struct cfg_t {
   int k1d = 0;        // dc == 3: the whole bank resident, input by 16-B LDS-DMA (bh_k1s.hip k1d_kernel)
   int k1w = 0;        // dc == 3: store waves of the k1w form (bh_k1s.hip k1w_kernel; NT counts them too)
   int k1w_sl = 0;     // k1w: LDS staging slots per compute wave
+  int k1r = 0;        // dc == 3: the bank slice in VGPRs, K <= k1r (bh_k1s.hip k1r_kernel)
 };
 
 // bh_ring.hip: LDS-DMA ring configurations (conv ones read the repacked filter bank) and

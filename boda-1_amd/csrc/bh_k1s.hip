@@ -939,6 +939,163 @@ cfg_t k1w_cfg(const char *name) {
   return c;
 }
 
+// compile-time loop: f(integral_constant<int, I>) for I in [I0, N) (register-array indices must be constants)
+template <int I, int N, class F>
+__device__ __forceinline__ void k1_static_for(F &&f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    k1_static_for<I + 1, N>(f);
+  }
+}
+
+// k1r_kernel (round 6, configs kr<OCT>k<KMAX>c<KC>q<Q>w<NW>): k1n (TN = 1) with the bank slice held in
+// VGPRs instead of LDS, for K <= KMAX (TM * KMAX / 2 registers: lane (li, kh) keeps bank rows 2 s + kh of
+// channels oc0 + 32 t + li). A wave loads its slice once (two 128-B row pieces per instruction) and
+// then never touches LDS: no fragment reads per MFMA, no bank DMA, no barrier -- waves are independent
+// from their first load. The chunk loop is unrolled over KMAX / KC chunks (register indices must be
+// compile-time) and stops at the op's K / KC; the input ring, the unit stream and the epilogue are
+// k1n's (the first unit's dropped stores keep every unit's VMEM sequence alike for the counted waits).
+template <int TM, int KMAX, int KC, int Q, int NW>
+__global__ __launch_bounds__(NW * 64) void k1r_kernel(GemmArgs p) {
+  constexpr int OCT = 32 * TM, SC = KC / 2, S = 16 * TM, NCH = KMAX / KC;
+  static_assert(TM >= 1 && TM <= 2 && KC % 2 == 0 && KMAX % (KC * Q) == 0, "tile");
+  static_assert(Q >= 2 && (Q - 1) * SC + S <= 63, "vmcnt range");
+  const int lane = threadIdx.x & 63, li = lane & 31, kh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t l8 = blockIdx.x >> 3;
+  const uint32_t oct = l8 % p.tiles_m;
+  const uint32_t gi = (l8 / p.tiles_m) * 8 + (blockIdx.x & 7);
+  const uint32_t wg = (gridDim.x / p.tiles_m) * NW;
+  const uint32_t oc0 = oct * OCT;
+  const uint32_t npu = (p.N + 31) / 32, nch = p.K / KC;
+  const uint32_t hw4 = p.HW * 4u, ohw4 = p.OHW * 4u;
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsx = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rso = make_rsrc(p.c, p.c_bytes);
+  const __amdgpu_buffer_rsrc_t rsbias = make_rsrc(p.bias, p.bias ? p.M * 4u : 0u);
+  uint32_t pu = gi * NW + (uint32_t)wave;
+  if (pu >= npu) return;
+
+  // the bank slice (rows past K and columns past the packed width: zeros) and the tile's biases as
+  // each unit's first C operand (row 8 g + 4 kh + e of tile t)
+  float wreg[TM][KMAX / 2];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const uint32_t col = oc0 + 32u * t + (uint32_t)li;
+    const uint32_t vo = oob_unless(col < p.lda, (kh * p.lda + col) * 4u);
+#pragma unroll
+    for (int s = 0; s < KMAX / 2; ++s)
+      wreg[t][s] = ldv<1>(rsw, oob_unless(2u * s < p.K, vo), 2u * s * p.lda * 4u);
+  }
+  f32x16 biasv[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t oc = oc0 + 32u * t + 8u * g + 4u * kh + e;
+        biasv[t][4 * g + e] = ldv<1>(rsbias, oob_unless(oc < p.M, oc * 4u), 0u);
+      }
+  auto ubase = [&](uint32_t u) -> uint32_t {
+    const uint32_t n = u * 32u + (uint32_t)li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    return oob_unless((u < npu) & (n < p.N), (img * p.ICHW + pix + kh * p.HW) * 4u);
+  };
+  float xr[Q][SC];
+  auto issue = [&](int q, uint32_t base, uint32_t c) {
+    const uint32_t vb = base + c * KC * hw4;
+#pragma unroll
+    for (int s = 0; s < SC; ++s) xr[q][s] = ldv<1>(rsx, vb, 2 * s * hw4);
+  };
+  uint32_t bcur = ubase(pu), bnext = ubase(pu + wg);
+#pragma unroll
+  for (int q = 0; q < Q - 1; ++q) issue(q, bcur, (uint32_t)q);
+#pragma unroll
+  for (int s = 0; s < S; ++s) __builtin_amdgcn_raw_buffer_store_b32(0u, rso, OOB, 0, 0);
+
+  f32x16 acc[TM];
+  const bool full_m = oc0 + OCT <= p.M;
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(p.res, p.res ? p.c_bytes : 0u);
+  const float floor0 = p.relu ? 0.0f : __builtin_nanf("");  // relu_floor: NaN = no clamp
+  auto epilogue = [&](auto masked, auto res, auto wt) {
+    uint32_t h4 = ohw4;
+    asm volatile("" : "+s"(h4));
+    const uint32_t so0 = oc0 * h4;
+    const uint32_t n = pu * 32u + (uint32_t)li;
+    const uint32_t img = fdiv(n, p.ohw_m, p.ohw_s), pix = n - img * p.OHW;
+    const uint32_t ob = oob_unless((pu < npu) & (n < p.N), (img * p.OCOHW + pix) * 4u + (uint32_t)(4 * kh) * h4);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t so = so0 + (uint32_t)(32 * t + 8 * g + i) * h4;
+          uint32_t o = ob;
+          if constexpr (decltype(masked)::value) o = oob_unless(oc0 + (uint32_t)(32 * t + 8 * g + 4 * kh + i) < p.M, ob);
+          float v = acc[t][4 * g + i];
+          if constexpr (decltype(res)::value) v += ldv<1>(rsr, o, so);
+          v = relu_floor(v, floor0);
+          if constexpr (decltype(wt)::value) stv<1, AUX_SC1>(v, rso, o, so);
+          else stv<1, AUX_OUT>(v, rso, o, so);
+        }
+  };
+  auto epilogue_m = [&](auto masked) {
+    if (p.res) {
+      if (p.wt) epilogue(masked, std::true_type{}, std::true_type{});
+      else epilogue(masked, std::true_type{}, std::false_type{});
+    } else {
+      if (p.wt) epilogue(masked, std::false_type{}, std::true_type{});
+      else epilogue(masked, std::false_type{}, std::false_type{});
+    }
+  };
+  for (;;) {
+    k1_static_for<0, NCH>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if ((uint32_t)c >= nch) return;
+      // chunks 0 .. Q - 2 of a unit were issued before the previous unit's S stores
+      if (c < Q - 1) vm_wait<(Q - 2) * SC + S>();
+      else vm_wait<(Q - 2) * SC>();
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const uint32_t c2 = (uint32_t)c + (uint32_t)(Q - 1);
+        const bool nx = c2 >= nch;
+        issue((c + Q - 1) % Q, nx ? bnext : bcur, nx ? c2 - nch : c2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < SC; ++s) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(wreg[t][c * SC + s], xr[c % Q][s],
+                                                         c == 0 && s == 0 ? biasv[t] : acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (full_m) epilogue_m(std::false_type{});
+    else epilogue_m(std::true_type{});
+    pu += wg;
+    if (pu >= npu) break;
+    bcur = bnext;
+    bnext = ubase(pu + wg);
+  }
+  vm_wait<0>();
+}
+
+template <int TM, int KMAX, int KC, int Q, int NW>
+cfg_t k1r_cfg(const char *name) {
+  cfg_t c{name, 32 * TM, 32 * NW, KC, 64 * NW, {}, 1};
+  c.k[A_KVEC][B_DIRECT][0] = k1r_kernel<TM, KMAX, KC, Q, NW>;
+  c.dc = 3;
+  c.dc_ky = 1;
+  c.dc_kx = 1;
+  c.dc_ci = KC;
+  c.dc_rin = Q;
+  c.k1r = KMAX;
+  return c;
+}
+
 template <int TM, int TN, int KC, int Q, int NW, int DBG = 0>
 cfg_t k1n_cfg(const char *name) {
   cfg_t c{name, 32 * TM, 32 * TN * NW, KC, 64 * NW, {}, 1};
@@ -1008,6 +1165,12 @@ std::vector<cfg_t> k1s_cfgs() {
       k1w_cfg<3, 16, 3, 4, 1, 1>("kw96c16q3w4s1l1"),
       k1w_cfg<3, 8, 12, 4, 1, 1>("kw96c8q12w4s1l1"), k1w_cfg<3, 16, 6, 4, 1, 1>("kw96c16q6w4s1l1"),
       k1w_cfg<1, 8, 12, 8, 2, 2>("kw32c8q12w8s2l2"),
+      // k1r <TM, KMAX, KC, Q, NW>: kr<OC tile>k<largest K>c<KC>q<Q>w<NW>, the bank slice in VGPRs
+      k1r_cfg<1, 64, 16, 4, 4>("kr32k64c16q4w4"),   k1r_cfg<1, 64, 16, 4, 8>("kr32k64c16q4w8"),
+      k1r_cfg<1, 96, 16, 3, 4>("kr32k96c16q3w4"),   k1r_cfg<1, 96, 16, 3, 8>("kr32k96c16q3w8"),
+      k1r_cfg<1, 96, 8, 4, 8>("kr32k96c8q4w8"),     k1r_cfg<1, 128, 16, 4, 4>("kr32k128c16q4w4"),
+      k1r_cfg<1, 192, 16, 3, 4>("kr32k192c16q3w4"), k1r_cfg<2, 64, 16, 4, 4>("kr64k64c16q4w4"),
+      k1r_cfg<2, 96, 16, 3, 4>("kr64k96c16q3w4"),
 #ifdef BH_KTRACE
       k1d_cfg<3, 32, 4, 4, 1>("xkd96c32d4w4_nostore"), k1d_cfg<3, 16, 6, 4, 1>("xkd96c16d6w4_nostore"),
       k1n_cfg<1, 1, 32, 3, 8, 1>("xkn32p32c32q3w8_nostore"), k1n_cfg<1, 1, 16, 4, 8, 1>("xkn32p32c16q4w8_nostore"),
@@ -1075,6 +1238,9 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   if (c.k1d) return launch_k1d(ctx, c, p, splits, first);
   if (p.K % KC || (p.K / KC) % Q)
     return bh::fail(BH_UNSUP, std::string("conv: input channels not a whole number of ") + c.name + " trips");
+  if (c.k1r && p.K > (uint32_t)c.k1r)
+    return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " holds at most " + std::to_string(c.k1r) +
+                                  " input channels in registers");
   // k1w: a store-wave lane's 4 pixels lie in one image and its 16-B output / residual accesses are aligned
   if (c.k1w && (p.OHW % 4 || (uintptr_t)p.c % 16 || (uintptr_t)p.res % 16))
     return bh::fail(BH_UNSUP, std::string("conv: ") + c.name + " needs OH*OW % 4 == 0 and 16-B aligned output rows");
@@ -1090,7 +1256,8 @@ int launch_k1s(bh_ctx *ctx, const cfg_t &c, GemmArgs &p, uint32_t B, uint32_t KY
   // k1w: the bank slice padded to whole 64-lane 16-B DMAs, the biases, c.k1w_sl [BM][32] staging slots per
   // compute wave and two counters per compute wave
   const uint32_t nw = NT / 64 - (uint32_t)c.k1w;  // compute waves
-  const uint64_t lds = c.k1w  ? (((uint64_t)p.K * c.BM / 4 + 63) / 64 * 256 + (uint64_t)((c.BM + 63) / 64) * 64 +
+  const uint64_t lds = c.k1r  ? 0
+                       : c.k1w  ? (((uint64_t)p.K * c.BM / 4 + 63) / 64 * 256 + (uint64_t)((c.BM + 63) / 64) * 64 +
                                 (uint64_t)nw * c.k1w_sl * c.BM * 32 + 2 * nw) * 4
                        : c.k1n ? ((uint64_t)p.K * c.BM + (uint64_t)((c.BM + 63) / 64) * 64) * 4
                                : ((uint64_t)p.K * c.BM + (uint64_t)(NT / 64) * 32 * 36) * 4;

@@ -38,7 +38,7 @@ CONV_SHAPES = [
 # gvp* only IC % 16 == 0: test_conv_gvp below; ks* (1x1): test_gpu_k1s.py; wg* (Winograd 3x3):
 # test_gpu_wino.py; wx* (position-split Winograd 3x3 / 5x5): test_gpu_wgx.py
 @pytest.mark.parametrize("ci", [i for i, n in enumerate(boda_hip.tune_cfg_names(1))
-                                if not n.startswith(("dc", "dm", "gvp", "gvs", "gvo", "fcv", "ks", "kn", "kd", "kw", "wg", "wx"))],
+                                if not n.startswith(("dc", "dm", "gvp", "gvs", "gvo", "fcv", "ks", "kn", "kd", "kw", "kr", "wg", "wx"))],
                          ids=lambda i: boda_hip.tune_cfg_names(1)[i])
 @pytest.mark.parametrize("splits", [1, 3, -3])
 def test_conv_config(dev, ci, splits):

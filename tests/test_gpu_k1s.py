@@ -1,5 +1,5 @@
 """Resident-bank 1x1 kernels (bh_k1s.hip, configs ks*, their pixels-on-N form kn*, the whole-bank kd* and the
-store-wave kw*) against the oracle.
+store-wave kw* and the register-bank kr*) against the oracle.
 
 Each ks / kn configuration serves unpadded stride-1 1x1 convs whose input channels are a whole
 number of its trips (Q chunks of KC channels: ks<OCT>c<KC>q<Q>, kn<OCT>p<pixels per unit>c<KC>q<Q>;
@@ -23,13 +23,13 @@ from test_gpu_conv import run_conv
 
 pytestmark = pytest.mark.gpu
 
-KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("ks", "kn", "kd", "kw"))]
+KS = [n for n in boda_hip.tune_cfg_names(1) if n.startswith(("ks", "kn", "kd", "kw", "kr"))]
 
 
 def trip_of(name):
     if name.startswith("kd"):  # kd<OCT>c<KC>d<D>w<NW>: K a multiple of KC (and >= (D - 1) KC: min_k)
         return int(re.match(r"kd\d+c(\d+)", name).group(1))
-    kc, q = map(int, re.match(r"k[snw]\d+(?:p\d+)?c(\d+)q(\d+)", name).groups())
+    kc, q = map(int, re.match(r"k[snwr]\d+(?:p\d+)?(?:k\d+)?c(\d+)q(\d+)", name).groups())
     return kc * q
 
 
@@ -50,7 +50,9 @@ def fits(name, ic, oc=None, ohw=None):
     """ks: the bank slice [IC][OCT] and the waves' [32][36] epilogue tiles fit the LDS; kn: the
     bank slice and the tile's biases (whole 64-float DMAs); kd: the whole bank [IC][OC rounded to
     the sub-tile], the biases and every wave's ring [D][KC][32], with OH*OW % 4 == 0."""
-    oct_ = int(re.match(r"k[sdnw](\d+)", name).group(1))
+    oct_ = int(re.match(r"k[sdnwr](\d+)", name).group(1))
+    if name.startswith("kr"):  # the bank slice in registers: K <= KMAX, no LDS
+        return ic <= int(re.match(r"kr\d+k(\d+)", name).group(1))
     if name.startswith("kw"):  # the bank slice in whole 64-lane 16-B DMAs, biases, staging slots, counters
         nw, nsl = map(int, re.match(r"kw\d+c\d+q\d+w(\d+)s\d+l(\d+)", name).groups())
         lds = -(-(ic * oct_ // 4) // 64) * 256 + -(-oct_ // 64) * 64 + nw * nsl * oct_ * 32 + 2 * nw
@@ -132,7 +134,7 @@ def test_ks_rejects(dev, cn):
 
 @pytest.mark.parametrize("cn,s", [(cn, s) for cn in ("ks96c32q3", "ks64c16q4", "kn96p32c8q4w8", "kn64p64c16q3w8",
                                                     "kn32p128c16q4w4", "kd96c16d6w4", "kd64c16d6w4", "kd32c32d5w4",
-                                                    "kw32c16q3w8s2l2", "kw96c8q4w4s1l1")
+                                                    "kw32c16q3w8s2l2", "kw96c8q4w4s1l1", "kr32k192c16q3w4")
                                   for s in (k1(2, 192, 14, 14, 96), k1(3, 192, 13, 13, 70), k1(2, 192, 12, 12, 72))
                                   if (s.OH * s.OW) % tn_of(cn) == 0])
 def test_ks_residual_and_slab(dev, cn, s):

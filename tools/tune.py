@@ -39,7 +39,7 @@ CFG_BK = {}
 
 def bk_of(name):
     """K tile depth of a config name like 128x128x32 or sk32x32x64w8."""
-    if name.startswith(("dc", "dm", "fcv", "ks", "kn", "kd", "kw", "wg", "wx")):
+    if name.startswith(("dc", "dm", "fcv", "ks", "kn", "kd", "kw", "kr", "wg", "wx")):
         return 1 << 30
     if name.startswith("gv"):
         m = re.search(r"w(\d+)", name)
@@ -271,7 +271,7 @@ def main():
                             if cn.endswith("k"):  # stream-K: + the separate combine kernel (splits 20)
                                 cand.append((ci, 20))
                         continue
-                    if cn.startswith(("ks", "kn", "kd", "kw")):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
+                    if cn.startswith(("ks", "kn", "kd", "kw", "kr")):  # resident-bank 1x1: S = blocks per CU; UNSUP for other ops
                         if kind == 1 and s.KY == s.KX == 1 and s.sy == s.sx == 1 and s.py == s.px == 0:
                             cand += [(ci, 1), (ci, 2), (ci, 8)]  # 8: one unit per wave
                         continue
